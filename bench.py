@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Benchmark: Msites/s of the POPBAM hot path (per-site consensus call + nucdiv + sfs + ld
+ZnS over 10 kb windows, 12 samples) on MI355X -- BASELINE.json configs[2]: synthetic 1 contig,
+50 Msites x 12 samples.
+
+One step = one pass of the hot path over one batch: the call kernel over every position of
+the HBM-resident synthetic pileup (reads -> packed rows) followed by the window-statistics
+kernel over all 4,999 windows.  Multi-GPU: one process per GPU (torchrun), each rank owns its
+own 50 Msite shard (its own seed), no collective on the data path (weak scaling); only the
+timing barrier and max-over-ranks reduction use torch.distributed.
+
+Prints one JSON line (rank 0).  `roofline` is for the dominant kernel (the call kernel):
+algorithmic bytes per launch / its mean duration measured with HIP events on the stream the
+kernel runs on.  `cpu_baseline` times the CPU oracle (C++ restatement of the reference
+path, one core) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+METRIC = "Msites/sec (nucdiv+sfs+ld, 10kb win, 12 samples) at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--sites", type=int, default=50_000_000, help="positions per GPU")
+    ap.add_argument("--samples", type=int, default=12)
+    ap.add_argument("--depth", type=int, default=10)
+    ap.add_argument("--window", type=int, default=10_000)
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xC0FFEE02)
+    ap.add_argument("--cpu-sample", type=int, default=60_000, help="positions for the CPU baseline (0 = skip)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle (kind 'port', 1 core): three separate runs -- nucdiv, sfs, ld -- as the
+    reference computes them, each re-calling every position, over the first --cpu-sample
+    positions of the same synthetic pileup."""
+    import numpy as np
+
+    import harness
+    from popbam_amd import workload
+
+    n, L = args.samples, args.cpu_sample
+    batch = harness.synth_batch(args.seed, 0, L, n, args.depth)
+    p = harness.oracle_params_from(workload.default_params(n))
+    lib = harness.oracle()
+    names = [f"s{i}".encode() for i in range(n)]
+    pops = [b"popA", b"popB"]
+    sn = (C.c_char_p * n)(*names)
+    pn = (C.c_char_p * 2)(*pops)
+    rd = np.ascontiguousarray(batch["reads"])
+    tot = 0.0
+    win = min(args.window, max(2, L // 4))
+    for cmd in (4, 6, 5):   # nucdiv, sfs, ld (popbam_func_t)
+        c = harness.OrcCmd()
+        c.cmd, c.output, c.min_sites, c.min_snps, c.min_freq = cmd, 0, 10, 10, 1
+        c.windowed, c.win_size, c.beg, c.end = 1, win, 0, L
+        c.chr_name = b"chr1"
+        c.sample_names = C.cast(sn, C.POINTER(C.c_char_p))
+        c.pop_names = C.cast(pn, C.POINTER(C.c_char_p))
+        buf = C.create_string_buffer(1 << 22)
+        t0 = time.perf_counter()
+        r = lib.orc_run(C.byref(p), C.byref(c), L, batch["ref"].ctypes.data, batch["depth"].ctypes.data,
+                        rd.ctypes.data, buf, 1 << 22)
+        tot += time.perf_counter() - t0
+        assert r >= 0
+    return {"value": round(L / tot / 1e6, 6), "unit": "Msites/s", "cores": 1, "kind": "port",
+            "sample": f"first {L} positions of the same synthetic pileup ({n} samples, depth {args.depth}); "
+                      f"oracle C++ restatement, nucdiv+sfs+ld as 3 separate passes (each re-calls all sites), "
+                      f"{win} bp windows; excludes BAM decode/pileup"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    from popbam_amd import _lib, workload
+
+    n = args.samples
+    params = workload.default_params(n)
+    ctx = _lib.Context(params, torch.cuda.current_device())
+    seed = args.seed + rank   # each rank: its own 50 Msite shard of the genome
+    syn = workload.SynthPileup(ctx, args.sites, args.depth, seed)
+    wins = workload.reference_windows(0, args.sites, args.window)
+    stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS
+    hp = workload.HotPath(ctx, syn, wins, stats)
+    stream = torch.cuda.current_stream()
+
+    for _ in range(args.warmup):
+        hp.step(stream)
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1, e2 in ev:
+        e0.record(stream)
+        hp.call(stream)
+        e1.record(stream)
+        hp.window_stats(stream)
+        e2.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    call_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
+    stats_ms = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
+    total_sites = args.sites * world * args.steps
+    value = total_sites / elapsed / 1e6
+    call_bytes = syn.bytes_read_by_call()
+    achieved = call_bytes / (call_ms * 1e-3) / 1e9
+    stats_bytes = args.sites * ctx.row_bytes
+
+    # per-launch HBM traffic from rocprofv3 PMC counters, when a profile of this code is committed
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_call_kernel.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                d = json.load(f)
+            if d.get("sites") == args.sites and d.get("samples") == n and d.get("depth") == args.depth:
+                traffic = d.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = None
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Msites/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (counter-based pileup resident in HBM, generated on device)",
+            "config": {"workload": "configs[2]: synthetic 1 contig x 50 Msites x 12 samples per GPU, "
+                                   "consensus call + nucdiv + sfs + ld(ZnS), 10 kb windows",
+                       "sites_per_gpu": args.sites, "samples": n, "mean_depth": args.depth,
+                       "window": args.window, "windows_per_gpu": len(wins), "reads_per_gpu": syn.n_reads,
+                       "parallelism": f"dp{world} (independent window-range shards, no collective)"},
+            "roofline": {"bound": "hbm", "kernel": "call_sites_kernel", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "bytes_per_launch": call_bytes, "ms_per_launch": round(call_ms, 4)},
+            "window_stats": {"ms_per_launch": round(stats_ms, 4), "rows_bytes": stats_bytes,
+                             "GBps": round(stats_bytes / (stats_ms * 1e-3) / 1e9, 2),
+                             "Msites_per_s_stats_only": round(args.sites / (stats_ms * 1e-3) / 1e6, 2)},
+        }
+        if world == 1 and args.cpu_sample > 0:
+            out["cpu_baseline"] = cpu_baseline(args)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,206 @@
+/* popbam_gpu.h -- C-ABI of the MI355X-native POPBAM hot path (libpopbam_gpu.so).
+ *
+ * Drop-in boundary.  The reference drives its hot path through the pileup callback
+ *     int (*bam_pileup_f)(uint32_t tid, uint32_t pos, int n, const bam_pileup1_t *pl, void *data)
+ * (bam.h:554), registered per window with bam_plbuf_init(make_<cmd>, &t)
+ * (bam_pileup.c:505-540) and implemented by make_nucdiv / make_sfs / make_ld / make_diverge /
+ * make_haplo / make_snp (e.g. pop_nucdiv.cpp:136-204), each of which runs
+ * popbamData::call_base (popbam.cpp:186-313) + clean_heterozygotes / segbase / qfilter
+ * (pop_utils.cpp:102-201) per position and then calc_<stat> / print_<stat> per window.
+ *
+ * This library replaces everything after the callback's per-sample partition:
+ *   - the host side of the callback (reference popbam.cpp:220-249: skip is_del /
+ *     is_refskip / BAM_FUNMAP, RG -> sample, keep the first max_depth reads per sample)
+ *     copies four bytes per kept read out of bam1_t into a dense pileup batch (pbg_pileup);
+ *   - pbg_call_sites()     = call_base from popbam.cpp:252 on + clean_heterozygotes +
+ *                            segbase + qfilter + cal_site_type + the make_<cmd> site store,
+ *                            producing one packed row per position;
+ *   - pbg_window_stats()   = calc_diff_matrix + calc_nucdiv / calc_sfs / calc_zns /
+ *                            calc_omegamax / calc_wall / calc_diverge / calc_nhaps /
+ *                            calc_ehhs / calc_minDxy over any list of windows;
+ * pbg_run() chains them for one `popbam <cmd>` invocation and prints the reference's TSV
+ * (print_<stat>, byte-identical); the CLI and the tests use it.
+ *
+ * Conventions: every entry point returns 0 on success or a negative PBG_E* code and never
+ * exits; pbg_last_error() has the message.  One context per device; calls on one context are
+ * not thread-safe.  Pointers documented "device" must be device (HBM) memory; the caller owns
+ * all buffers it passes; the context owns its tables and scratch.  `stream` is a hipStream_t
+ * (NULL = default stream); asynchronous entry points only enqueue work on it.
+ */
+#ifndef POPBAM_GPU_H
+#define POPBAM_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBG_MAX_SAMPLES 64     /* u64 masks, as the reference (popbam.1:507-510)        */
+#define PBG_MAX_POPS    16
+#define PBG_SITE_BLOCK  64     /* positions per pbg_pileup.block_off entry                 */
+
+#define PBG_OK           0
+#define PBG_E_ARG       -1
+#define PBG_E_HIP       -2
+#define PBG_E_NOMEM     -3
+#define PBG_E_RANGE     -4
+#define PBG_E_NODEV     -5
+
+/* BAM_* option bits, same values as popbam.h:59-94 */
+#define PBG_F_ILLUMINA     0x02
+#define PBG_F_SUBSTITUTE   0x10
+#define PBG_F_HETEROZYGOTE 0x20
+#define PBG_F_OUTGROUP     0x40
+
+typedef struct pbg_ctx pbg_ctx;
+
+/* Sample model + calling filters (popbamData members, popbam.h:236-264; defaults
+ * popbam.cpp:79-93). */
+typedef struct {
+    int32_t  n_samples;                 /* sm->n, 1..PBG_MAX_SAMPLES                     */
+    int32_t  n_pops;                    /* sm->npops, 1..PBG_MAX_POPS                    */
+    uint64_t pop_mask[PBG_MAX_POPS];    /* assign_pops (popbam.cpp:145-171)              */
+    int32_t  pop_n[PBG_MAX_POPS];       /* pop_nsmpl                                      */
+    int32_t  min_depth, max_depth;      /* -m -x                                          */
+    int32_t  min_rmsQ, min_snpQ;        /* -q -s                                          */
+    int32_t  min_mapQ, min_baseQ;       /* -a -b (unsigned char in the reference)         */
+    uint32_t flag;                      /* PBG_F_* bits                                   */
+} pbg_params;
+
+/* Dense pileup batch for contiguous positions [pos0, pos0 + n_sites) of one contig.
+ * All pointers are DEVICE pointers.
+ *   ref[i]        reference base byte (faidx_fetch_seq); bit 7 set = the pileup made no
+ *                 callback at this position (no mask-passing read covers it)
+ *   depth[i*n+s]  kept reads of sample s at position i (after the max_depth cap)
+ *   block_off[b]  index in reads[] of the first read of position b*PBG_SITE_BLOCK;
+ *                 ceil(n_sites/PBG_SITE_BLOCK)+1 entries, last = total reads
+ *   reads[]       one u32 per kept read, (position, sample, pileup order) major:
+ *                 bits 0-7 bam1_qual()[qpos], 8-15 core.qual (mapQ),
+ *                 16-19 bam1_seqi(seq, qpos) (nt16), bit 20 bam1_strand()            */
+typedef struct {
+    uint32_t        n_sites;
+    int32_t         pos0;
+    const uint8_t  *ref;
+    const uint16_t *depth;
+    const uint64_t *block_off;
+    const uint32_t *reads;
+} pbg_pileup;
+
+/* Row format written by pbg_call_sites: one little-endian word of W = 8*pbg_row_bytes()
+ * bits per position (2 B for n<=14, 4 B for n<=30, 8 B for n<=62, 16 B for n<=64):
+ *   bits 0..n-1  cal_site_type: sample derived & passing ((cb&3)==3)
+ *   bit  W-2     counted: all n samples pass qfilter (popcount(sample_cov)==n)
+ *   bit  W-1     segregating: counted and segbase() > 0
+ * A position that is not counted has row 0.                                            */
+
+typedef struct { int32_t beg, end; } pbg_window;   /* row index range [beg, end)           */
+
+/* statistics selectable in pbg_window_stats */
+#define PBG_S_NUCDIV   0x001   /* pi / dxy              (pop_nucdiv.cpp:206-256)      */
+#define PBG_S_SFS      0x002   /* Tajima D, Fay-Wu H    (pop_sfs.cpp:227-291)         */
+#define PBG_S_ZNS      0x004   /* ld -o 0               (pop_ld.cpp:201-252)          */
+#define PBG_S_OMEGA    0x008   /* ld -o 1               (pop_ld.cpp:254-373)          */
+#define PBG_S_WALL     0x010   /* ld -o 2               (pop_ld.cpp:375-458)          */
+#define PBG_S_DIV_IND  0x020   /* diverge -o 0          (pop_diverge.cpp:228-231)     */
+#define PBG_S_DIV_POP  0x040   /* diverge -o 1          (pop_diverge.cpp:232-253)     */
+#define PBG_S_HAP_K    0x080   /* haplo -o 0            (pop_haplo.cpp:208-254)       */
+#define PBG_S_HAP_EHHS 0x100   /* haplo -o 1            (pop_haplo.cpp:256-323)       */
+#define PBG_S_HAP_DXY  0x200   /* haplo -o 2            (pop_haplo.cpp:325-363)       */
+
+typedef struct {
+    uint32_t stats;        /* PBG_S_* mask                                                */
+    int32_t  min_freq;     /* ld: 1, or 2 with -e                                         */
+    int32_t  outidx;       /* sfs/diverge outgroup sample (-p) when PBG_F_OUTGROUP is set  */
+    int32_t  jc;           /* diverge -d jc                                                */
+} pbg_stat_opts;
+
+/* Per-window results (DEVICE arrays, caller-allocated, NULL = not wanted).  Values are the
+ * exact numbers the reference prints (already divided by num_sites where it divides). */
+typedef struct {
+    int32_t  *num_sites;   /* [n_win]                                                    */
+    int32_t  *segsites;    /* [n_win]                                                    */
+    double   *pi;          /* [n_win*n_pops]            nucdiv pi (piw/num_sites)         */
+    double   *dxy;         /* [n_win*n_pops*(n_pops-1)] nucdiv dxy, reference indexing    */
+    double   *td, *fwh;    /* [n_win*n_pops]            sfs                               */
+    int32_t  *ld_snps;     /* [n_win*n_pops]            ld S[] column                     */
+    double   *ld_val;      /* [n_win*n_pops]            ZnS / omega_max / Wall B          */
+    double   *ld_q;        /* [n_win*n_pops]            Wall Q                            */
+    double   *div_ind;     /* [n_win*n_samples]         diverge -o 0 distance             */
+    int32_t  *div_fixed;   /* [n_win*n_pops]            diverge -o 1 Fixed (u16 wrap)     */
+    int32_t  *div_seg;     /* [n_win*n_pops]            diverge -o 1 Seg                  */
+    double   *div_pop;     /* [n_win*n_pops]            diverge -o 1 distance             */
+    int32_t  *nhaps;       /* [n_win*n_pops]            haplo K                           */
+    double   *hap_val;     /* [n_win*n_pops]            haplo Kdiv (1-hdiv) / EHHS / pi   */
+    double   *hap_dxy;     /* [n_win*n_pops*(n_pops-1)] haplo -o 2 dxy                    */
+    int32_t  *hap_min;     /* [n_win*n_pops*(n_pops-1)] haplo -o 2 min (u16)              */
+} pbg_window_out;
+
+/* ---- context ---------------------------------------------------------------------- */
+int         pbg_create(pbg_ctx **ctx, int device, const pbg_params *params);
+void        pbg_destroy(pbg_ctx *ctx);
+const char *pbg_last_error(const pbg_ctx *ctx);   /* ctx may be NULL (last create error)  */
+int         pbg_row_bytes(const pbg_ctx *ctx);
+int         pbg_device_count(void);
+
+/* ---- hot path --------------------------------------------------------------------- */
+/* rows: device, n_sites * pbg_row_bytes(); cb: device u64[n_sites*n_samples] or NULL
+ * (final consensus words, layout pop_utils.cpp:6-24, for the snp subcommand).           */
+int pbg_call_sites(pbg_ctx *ctx, const pbg_pileup *pileup, void *rows, uint64_t *cb, void *stream);
+
+/* The staging capacity of pbg_call_sites (from block_off's last entry) and the workspace
+ * plan of pbg_window_stats (from the window list) are computed on the first call and cached
+ * per (device pointer, size): steady-state calls on a resident batch enqueue kernels only.
+ * A caller that rewrites a window list in place with a different layout must pass a new
+ * pointer (or n_win / n_rows) to force a new plan. */
+int pbg_window_stats(pbg_ctx *ctx, const void *rows, uint32_t n_rows, const pbg_window *wins,
+                     uint32_t n_win, const pbg_stat_opts *opts, const pbg_window_out *out,
+                     void *stream);
+
+/* ---- one subcommand end to end ------------------------------------------------------ */
+enum { PBG_CMD_SNP = 0, PBG_CMD_HAPLO = 1, PBG_CMD_DIVERGE = 2, PBG_CMD_NUCDIV = 4,
+       PBG_CMD_LD = 5, PBG_CMD_SFS = 6 };   /* popbam_func_t values (popbam.h:208)       */
+
+typedef struct {
+    int32_t  cmd;          /* PBG_CMD_*                                                   */
+    int32_t  output;       /* -o                                                          */
+    int32_t  min_sites;    /* -k                                                          */
+    int32_t  min_snps;     /* ld -n                                                       */
+    int32_t  min_freq;     /* ld 1 / 2 (-e)                                               */
+    int32_t  outidx;       /* -p sample index                                             */
+    int32_t  jc;           /* diverge -d jc                                               */
+    int32_t  windowed;     /* -w given                                                    */
+    int64_t  win_size;     /* bases                                                       */
+    int32_t  beg, end;     /* parsed region [beg, end) in contig coordinates              */
+    const char *chr_name;
+    const char *const *sample_names;
+    const char *const *pop_names;
+} pbg_cmd;
+
+/* Runs `popbam <cmd>` over a HOST pileup batch that covers contig positions
+ * [pileup->pos0, pileup->pos0 + n_sites) (host pointers; block_off may be NULL and is then
+ * derived from depth[]).  Writes the reference's stdout (TSV) into out (NUL-terminated).
+ * Returns the text length, or PBG_E_RANGE with *needed set when cap is too small.        */
+long pbg_run(pbg_ctx *ctx, const pbg_cmd *cmd, const pbg_pileup *host_pileup, char *out,
+             size_t cap, size_t *needed);
+
+/* print_<stat> for windows whose results were copied to the HOST: `host_out` holds host
+ * arrays laid out as pbg_window_out, `wbeg`/`wend` the contig coordinates the reference
+ * prints (+1 applied here).  Same return convention as pbg_run.                          */
+long pbg_format(const pbg_ctx *ctx, const pbg_cmd *cmd, const pbg_window_out *host_out, uint32_t n_win,
+                const int32_t *wbeg, const int32_t *wend, char *out, size_t cap, size_t *needed);
+
+/* ---- synthetic workload (benchmark) ------------------------------------------------- */
+/* Counter-based pileup generator (splitmix64 keyed on (seed, position)), written straight
+ * into device memory: pbg_synth_depth() fills ref/depth/block_off and reports the read
+ * count so the caller can allocate `reads` for pbg_synth_reads().  Device pointers.                  */
+int pbg_synth_depth(pbg_ctx *ctx, uint64_t seed, int32_t mean_depth, uint32_t n_sites,
+                    uint8_t *ref, uint16_t *depth, uint64_t *block_off, uint64_t *n_reads,
+                    void *stream);
+int pbg_synth_reads(pbg_ctx *ctx, uint64_t seed, int32_t mean_depth, uint32_t n_sites,
+                    const uint16_t *depth, const uint64_t *block_off, uint32_t *reads,
+                    void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POPBAM_GPU_H */

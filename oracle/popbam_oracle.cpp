@@ -1,0 +1,942 @@
+// popbam_oracle.cpp -- CPU restatement of the POPBAM 0.3 hot path (TEST INFRASTRUCTURE).
+//
+// Header comment of popbam_oracle.h applies: only tests/, smoke() and bench.py's
+// cpu_baseline leg use this, as the checker.  Every function cites the reference
+// file:line it restates (paths relative to /root/reference).  Quirks (SURVEY.md
+// Appendix A) are reproduced on purpose.  Pinned against the golden TSVs in tests/golden.
+//
+// Build: g++ -std=c++17 -O2 -ffp-contract=off (x86-64 SSE math, like the reference's -O2).
+
+#include "popbam_oracle.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <list>
+#include <string>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------- lookup tables
+// bam_nt16 -> nt4 (popbam.cpp:9); IUPAC genotype letters (popbam.cpp:11);
+// iupac_rev: A/a->0 C/c->1 G/g->2 T/t->3 else 14 (popbam.cpp:33-51).
+const int kNt16Nt4[16] = {4, 0, 1, 4, 2, 4, 4, 4, 3, 4, 4, 4, 4, 4, 4, 4};
+const char kIupac[16] = {'A', 'M', 'R', 'W', 'N', 'C', 'S', 'Y', 'N', 'N', 'G', 'K', 'N', 'N', 'N', 'T'};
+inline unsigned char iupac_rev(unsigned char c) {
+    switch (c) {
+        case 'A': case 'a': return 0;
+        case 'C': case 'c': return 1;
+        case 'G': case 'g': return 2;
+        case 'T': case 't': return 3;
+        default: return 14;
+    }
+}
+// "=ACMGRSVTWYHKDBN"[bam_nt16_table[c]] for the characters iupac[] can hold
+inline char nt16_char(unsigned char c) {
+    static const char rev[] = "=ACMGRSVTWYHKDBN";
+    int v = 15;
+    switch (c & 0xDF) {  // upper-case
+        case 'A': v = 1; break; case 'C': v = 2; break; case 'M': v = 3; break; case 'G': v = 4; break;
+        case 'R': v = 5; break; case 'S': v = 6; break; case 'V': v = 7; break; case 'T': v = 8; break;
+        case 'W': v = 9; break; case 'Y': v = 10; break; case 'H': v = 11; break; case 'K': v = 12; break;
+        case 'D': v = 13; break; case 'B': v = 14; break; case 'N': v = 15; break;
+        default: v = 15;
+    }
+    if (c == '=') v = 0;
+    return rev[v];
+}
+
+inline unsigned popcnt64(uint64_t x) { return (unsigned)__builtin_popcountll(x); }
+
+// ---------------------------------------------------------------- LogGamma
+// gamma.cpp:126-166 (and Gamma, gamma.cpp:11-124).  cal_coef only calls it at integer
+// x in [1, 256]; for x < 12 Gamma() reduces an integer argument to y == 1 (so the rational
+// approximation returns exactly 1.0) and multiplies up y, y+1, ..., i.e. computes
+// (x-1)! by repeated multiplication; for x >= 12 the Abramowitz-Stegun 6.1.41 series.
+double log_gamma_int(double x) {
+    if (x < 12.0) {
+        double y = x;
+        int n = static_cast<int>(std::floor(y)) - 1;
+        y -= n;                     // == 1.0 for integer x >= 1
+        double result = 1.0;        // num/den + 1.0 with z == 0
+        for (int i = 0; i < n; i++) result *= y++;
+        return std::log(std::fabs(result));
+    }
+    static const double c[8] = {1.0 / 12.0, -1.0 / 360.0, 1.0 / 1260.0, -1.0 / 1680.0,
+                                1.0 / 1188.0, -691.0 / 360360.0, 1.0 / 156.0, -3617.0 / 122400.0};
+    double z = 1.0 / (x * x);
+    double sum = c[7];
+    for (int i = 6; i >= 0; i--) {
+        sum *= z;
+        sum += c[i];
+    }
+    double series = sum / x;
+    static const double halfLogTwoPi = 0.91893853320467274178032973640562;
+    return (x - 0.5) * std::log(x) - x + halfLogTwoPi + series;
+}
+
+// ---------------------------------------------------------------- cal_coef
+// pop_utils.cpp:203-255, called through errmod_init(1.0-0.83) (pop_nucdiv.cpp:34):
+// the float parameter narrows 0.17 (pop_utils.cpp:257).
+struct Tables {
+    std::vector<double> fk, beta, lhet;
+    Tables() : fk(256), beta(256 * 256 * 64), lhet(256 * 256) {
+        const double depcorr = (double)(float)(1.0 - 0.83);
+        const double eta = 0.03;
+        const double kLn2 = 0.69314718055994530942, kLn10 = 2.30258509299404568402;
+        fk[0] = 1.0;
+        for (int n = 1; n != 256; ++n) fk[n] = std::pow(1.0 - depcorr, n) * (1.0 - eta) + eta;
+        std::vector<double> lC(256 * 256, 0.0);
+        for (int n = 1; n != 256; ++n) {
+            double lgn = log_gamma_int(n + 1);
+            for (int k = 1; k <= n; ++k) lC[n << 8 | k] = lgn - log_gamma_int(k + 1) - log_gamma_int(n - k + 1);
+        }
+        for (int q = 1; q != 64; ++q) {
+            double e = std::pow(10.0, -q / 10.0);
+            double le = std::log(e);
+            double le1 = std::log(1.0 - e);
+            for (int n = 1; n <= 255; ++n) {
+                double *b = beta.data() + (q << 16 | n << 8);
+                long double sum, sum1;
+                sum1 = sum = 0.0;
+                for (int k = n; k >= 0; --k, sum1 = sum) {
+                    sum = sum1 + expl(lC[n << 8 | k] + k * le + (n - k) * le1);
+                    b[k] = -10.0 / kLn10 * logl(sum1 / sum);
+                }
+            }
+        }
+        for (int n = 0; n < 256; ++n)
+            for (int k = 0; k < 256; ++k) lhet[n << 8 | k] = lC[n << 8 | k] - kLn2 * n;
+    }
+};
+const Tables &tables() {
+    static Tables t;
+    return t;
+}
+
+// ---------------------------------------------------------------- errmod_cal
+// pop_utils.cpp:280-365.  keys: qual:6 (<<5) | strand:1 (<<4) | base (low 4 bits).
+void errmod_cal(unsigned short n, unsigned short *bases, float *q) {
+    const Tables &T = tables();
+    double bsum[16] = {0};   // aux.fsum only feeds the dead bar_e; omitted
+    unsigned c[16] = {0};
+    int w[32] = {0};
+    std::memset(q, 0, 16 * sizeof(float));
+    if (n == 0) return;
+    if (n > 255) {
+        // ks_shuffle (ksort.h:254-262): j = (rand()/RAND_MAX)*i is integer division, 0
+        // except when rand() == RAND_MAX; every step swaps a[0] with a[i-1].
+        for (int i = n; i > 1; --i) std::swap(bases[0], bases[i - 1]);
+        n = 255;
+    }
+    std::sort(bases, bases + n);  // ks_introsort: ascending, result independent of algorithm
+    for (int j = n - 1; j >= 0; --j) {
+        unsigned short b = bases[j];
+        int qq = b >> 5 < 4 ? 4 : b >> 5;
+        if (qq > 63) qq = 63;
+        int k = b & 0x1f;
+        bsum[k & 0xf] += T.fk[w[k]] * T.beta[qq << 16 | n << 8 | c[k & 0xf]];
+        ++c[k & 0xf];
+        ++w[k];
+    }
+    const int m = 4;
+    for (int j = 0; j != m; ++j) {
+        float tmp1;
+        int tmp2;
+        tmp1 = 0.0f;
+        tmp2 = 0;
+        for (int k = 0; k != m; ++k) {
+            if (k == j) continue;
+            tmp1 += bsum[k];
+            tmp2 += c[k];
+        }
+        if (tmp2) q[j * m + j] = tmp1;
+        for (int k = j + 1; k < m; ++k) {
+            int cjk = c[j] + c[k];
+            tmp2 = 0;
+            tmp1 = 0.0f;
+            for (int i = 0; i < m; ++i) {
+                if (i == j || i == k) continue;
+                tmp1 += bsum[i];
+                tmp2 += c[i];
+            }
+            if (tmp2)
+                q[j * m + k] = q[k * m + j] = -4.343 * T.lhet[cjk << 8 | c[k]] + tmp1;
+            else
+                q[j * m + k] = q[k * m + j] = -4.343 * T.lhet[cjk << 8 | c[k]];
+        }
+        for (int k = 0; k != m; ++k)
+            if (q[j * m + k] < 0.0) q[j * m + k] = 0.0;
+    }
+}
+
+// ---------------------------------------------------------------- gl2cns  pop_utils.cpp:66-100
+uint64_t gl2cns(const float q[16], unsigned short k) {
+    unsigned short min_ij = 0;
+    float mn = FLT_MAX, mn_next = FLT_MAX;
+    for (int i = 0; i < 4; ++i)
+        for (int j = i; j < 4; ++j) {
+            float l = q[i << 2 | j];
+            if (l < mn) {
+                min_ij = (unsigned short)(i << 2 | j);
+                mn_next = mn;
+                mn = l;
+            } else if (l < mn_next) {
+                mn_next = l;
+            }
+        }
+    uint64_t snpq = (uint64_t)((mn_next - mn) + 0.499) << 32;
+    uint64_t nr = (uint64_t)k << 16;
+    uint64_t g = (uint64_t)min_ij << 8;
+    return snpq + nr + g;
+}
+
+// x86-64 gcc double -> unsigned long long: NaN yields 0x8000000000000000 (cvttsd2si
+// "indefinite" path), which the later <<48 discards.
+inline uint64_t d2u64(double d) {
+    if (std::isnan(d)) return 0x8000000000000000ULL;
+    return (uint64_t)d;
+}
+
+// ---------------------------------------------------------------- call_base  popbam.cpp:186-313
+// reads already partitioned per sample with the max_depth cap (popbam.cpp:220-249 is the
+// host side of the boundary); this is the per-sample part from popbam.cpp:252 on.
+void call_base(const orc_params *p, const uint16_t *depth, const uint32_t *reads, uint64_t *cb) {
+    std::vector<unsigned short> bases;
+    for (int j = 0; j < p->n_samples; ++j) {
+        cb[j] = 0;
+        int dj = depth[j];
+        if (dj == 0) continue;
+        bases.assign(dj, 0);
+        int rmsq = 0;
+        unsigned short k = 0;
+        for (int i = 0; i < dj; ++i) {
+            uint32_t r = reads[i];
+            int tmp_baseQ = r & 0xff;
+            int baseQ = (p->flag & 0x02) ? (tmp_baseQ > 31 ? tmp_baseQ - 31 : 0) : tmp_baseQ;
+            int mapQ = (r >> 8) & 0xff;
+            if (baseQ < p->min_baseQ || mapQ < p->min_mapQ) continue;
+            int b = kNt16Nt4[(r >> 16) & 0xf];
+            if (b > 3) continue;
+            int qq = baseQ < mapQ ? baseQ : mapQ;
+            if (qq < 4) qq = 4;
+            if (qq > 63) qq = 63;
+            bases[k++] = (unsigned short)(qq << 5 | ((r >> 20) & 1) << 4 | b);
+            rmsq += mapQ * mapQ;
+        }
+        reads += dj;
+        float q[16];
+        errmod_cal(k, bases.data(), q);
+        uint64_t rms = d2u64((double)std::sqrt((float)rmsq / k) + 0.499);
+        cb[j] = gl2cns(q, k);
+        cb[j] |= rms << 48;
+    }
+}
+
+// ---------------------------------------------------------------- clean_heterozygotes  pop_utils.cpp:170-201
+void clean_heterozygotes(int n, uint64_t *cb, int ref, int min_snpq) {
+    for (int i = 0; i < n; ++i) {
+        unsigned char g = (cb[i] >> 8) & 0xff;
+        unsigned char a1 = (g >> 2) & 0x3, a2 = g & 0x3;
+        unsigned short sq = (cb[i] >> 32) & 0xffff;
+        unsigned char r = iupac_rev((unsigned char)ref);
+        int d = (int)a2 - (int)a1;
+        if (a1 != a2 && sq >= min_snpq) {
+            if (a1 == r) cb[i] += (uint64_t)(int64_t)(d * (1 << 10));
+            if (a2 == r) cb[i] -= (uint64_t)(int64_t)(d * (1 << 8));
+        }
+        if (a1 != a2 && sq < min_snpq) {
+            if (a1 != r) cb[i] += (uint64_t)(int64_t)(d * (1 << 10));
+            if (a2 != r) cb[i] -= (uint64_t)(int64_t)(d * (1 << 8));
+        }
+    }
+}
+
+// ---------------------------------------------------------------- segbase  pop_utils.cpp:122-168
+int segbase(int n, uint64_t *cb, char ref, int min_snpq) {
+    int baseCount[4] = {0, 0, 0, 0};
+    for (int i = 0; i < n; ++i) {
+        unsigned char g = (cb[i] >> 8) & 0xff;
+        unsigned char a1 = (g >> 2) & 0x3, a2 = g & 0x3;
+        unsigned short sq = (cb[i] >> 32) & 0xffff;
+        if (a1 == a2 && kIupac[g] != ref && sq >= min_snpq) {
+            cb[i] |= 0x2ULL;
+            ++baseCount[a1];
+        } else if (a1 == a2 && kIupac[g] != ref && sq < min_snpq) {
+            // revert to the reference; the second subtraction borrows (Appendix A.3)
+            int d = (int)g - (int)iupac_rev((unsigned char)ref);
+            cb[i] -= (uint64_t)(int64_t)(d * (1 << 8));
+            cb[i] -= (uint64_t)(int64_t)(d * (1 << 10));
+        }
+    }
+    int j = 0, k = 0;
+    for (int i = 0; i < 4; ++i)
+        if (baseCount[i] > 0) { ++j; k = i; }
+    return j > 1 ? -1 : baseCount[k];
+}
+
+// ---------------------------------------------------------------- qfilter  pop_utils.cpp:102-120
+uint64_t qfilter(int n, uint64_t *cb, int min_rmsQ, int min_depth, int max_depth) {
+    uint64_t cov = 0;
+    for (int i = 0; i < n; ++i) {
+        unsigned short rms = (cb[i] >> 48) & 0xffff;
+        unsigned short nr = (cb[i] >> 16) & 0xffff;
+        if (rms >= min_rmsQ && nr >= min_depth && nr <= max_depth) {
+            cb[i] |= 0x1ULL;
+            cov |= 0x1ULL << i;
+        }
+    }
+    return cov;
+}
+
+// ---------------------------------------------------------------- per-window state (hData_t)
+struct Window {
+    int beg = 0, end = 0, num_sites = 0, segsites = 0;
+    std::vector<uint64_t> types;               // popbamData::types, per counted site
+    std::vector<std::vector<uint64_t>> seq;    // hap.seq[sample][word]
+    std::vector<unsigned> idx, pos;            // hap.idx / hap.pos per seg site
+    std::vector<std::vector<uint16_t>> snpq, rms, nreads;
+    std::vector<std::vector<unsigned char>> gbyte;
+    std::vector<char> refc;
+};
+
+struct Out {
+    std::string s;
+    void str(const char *x) { s += x; }
+    void str(const std::string &x) { s += x; }
+    void i(long long v) { s += std::to_string(v); }
+    void f(double v) {  // std::fixed << std::setprecision(5)
+        char b[512];
+        std::snprintf(b, sizeof b, "%.5f", v);
+        s += b;
+    }
+    void na() { s += "     NA"; }  // std::setw(7) << "NA"
+};
+
+std::string popname(const orc_cmd *c, int i) { return c->pop_names[i]; }
+
+// calc_diff_matrix pop_nucdiv.cpp:242-256 (same in pop_haplo.cpp:444-458): u16 wrap
+std::vector<std::vector<uint16_t>> diff_matrix(const orc_params *p, const Window &W) {
+    int n = p->n_samples;
+    std::vector<std::vector<uint16_t>> d(n, std::vector<uint16_t>(n, 0));
+    int words = (W.segsites - 1) / 64;  // SEG_IDX (popbam.h:124), C truncation
+    for (int i = 0; i < n - 1; i++)
+        for (int j = i + 1; j < n; j++) {
+            for (int k = 0; k <= words; k++) d[j][i] += popcnt64(W.seq[i][k] ^ W.seq[j][k]);
+            d[i][j] = d[j][i];
+        }
+    return d;
+}
+
+void head(Out &o, const orc_cmd *c, const Window &W) {
+    o.str(c->chr_name); o.str("\t"); o.i(W.beg + 1); o.str("\t"); o.i(W.end + 1); o.str("\t"); o.i(W.num_sites);
+}
+
+// ---- nucdiv: calc_nucdiv pop_nucdiv.cpp:206-239, print_nucdiv 258-289
+void do_nucdiv(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
+    int np = p->n_pops, n = p->n_samples;
+    auto d = diff_matrix(p, W);
+    std::vector<double> piw(np, 0.0), pib(np * (np - 1) > 0 ? np * (np - 1) : 1, 0.0);
+    for (int i = 0; i < np; i++)
+        for (int j = i; j < np; j++) {
+            for (int v = 0; v < n - 1; v++)
+                for (int w = v + 1; w < n; w++)
+                    if ((p->pop_mask[i] >> v & 1) && (p->pop_mask[j] >> w & 1)) {
+                        if (i == j) piw[i] += (double)d[v][w];
+                        else pib[i * np + (j - (i + 1))] += (double)d[v][w];
+                    }
+            if (i != j)
+                pib[i * np + (j - (i + 1))] *= 1.0 / (double)(p->pop_n[i] * p->pop_n[j]);
+            else {
+                piw[i] *= 2.0 / (double)(p->pop_n[i] * (p->pop_n[i] - 1));
+                if (std::isnan(piw[i])) piw[i] = 0.;
+            }
+        }
+    head(o, c, W);
+    for (int i = 0; i < np; i++) {
+        o.str("\tpi[" + popname(c, i) + "]:\t");
+        if (W.num_sites >= c->min_sites) o.f(piw[i] / W.num_sites); else o.na();
+    }
+    for (int i = 0; i < np - 1; i++)
+        for (int j = i + 1; j < np; j++) {
+            o.str("\tdxy[" + popname(c, i) + "-" + popname(c, j) + "]:\t");
+            if (W.num_sites >= c->min_sites) o.f(pib[i * np + (j - (i + 1))] / W.num_sites); else o.na();
+        }
+    o.str("\n");
+}
+
+// ---- sfs: calc_a1..e2 pop_sfs.cpp:511-571, calc_sfs 227-291, print_sfs 293-317
+struct SfsConst { std::vector<double> a1, a2, e1, e2; };
+SfsConst sfs_const(int n) {
+    SfsConst k;
+    k.a1.assign(n + 1, 0); k.a2.assign(n + 2, 0); k.e1.assign(n + 1, 0); k.e2.assign(n + 1, 0);
+    k.a1[0] = k.a1[1] = 1.0;
+    for (int i = 2; i <= n; i++) { k.a1[i] = 0; for (int j = 1; j < i; j++) k.a1[i] += 1.0 / (double)(j); }
+    k.a2[0] = k.a2[1] = 1.0;
+    for (int i = 2; i <= n + 1; i++) { k.a2[i] = 0; for (int j = 1; j < i; j++) k.a2[i] += 1.0 / (double)(j * j); }
+    k.e1[0] = k.e1[1] = 1.0;
+    for (int i = 2; i <= n; i++) {
+        double b1 = (i + 1.0) / (3.0 * (i - 1));
+        k.e1[i] = (b1 - (1.0 / k.a1[i])) / k.a1[i];
+    }
+    k.e2[0] = k.e2[1] = 1.0;
+    for (int i = 2; i <= n; i++) {
+        double b2 = (2.0 * (i * i + i + 3.0)) / (9.0 * i * (i - 1));
+        k.e2[i] = (b2 - ((i + 2.0) / (k.a1[i] * i)) + (k.a2[i] / (k.a1[i] * k.a1[i]))) / ((k.a1[i] * k.a1[i]) + k.a2[i]);
+    }
+    return k;
+}
+
+void do_sfs(Out &o, const orc_params *p, const orc_cmd *c, const Window &W, const SfsConst &K) {
+    int np = p->n_pops;
+    std::vector<double> td(np, 0.0), fwh(np, 0.0);
+    std::vector<int> num_snps(np, 0);
+    for (int i = 0; i < np; i++) {
+        std::vector<int> sfs(p->pop_n[i] + 1, 0);
+        for (int j = 0; j < W.segsites; j++) {
+            uint64_t t = W.types[W.idx[j]];
+            uint64_t pt = t & p->pop_mask[i];
+            unsigned short freq;
+            if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(p->pop_n[i] - popcnt64(pt));
+            else freq = (unsigned short)popcnt64(pt);
+            ++sfs[freq];
+            if (freq > 0 && freq < p->pop_n[i]) ++num_snps[i];
+        }
+        int n = p->pop_n[i];
+        int S = num_snps[i];
+        if (S > 0 && n > 1) {
+            const double *a1 = K.a1.data(), *a2 = K.a2.data(), *e1 = K.e1.data(), *e2 = K.e2.data();
+            for (int j = 1; j < n; j++) {
+                td[i] += sfs[j] * (((2.0 * j * (n - j)) / (n * (n - 1))) - (1.0 / a1[n]));
+                fwh[i] += sfs[j] * ((1.0 / a1[n]) - ((double)j / (n - 1)));
+            }
+            td[i] /= std::sqrt(e1[n] * S + e2[n] * S * (S - 1));
+            fwh[i] /= std::sqrt(((n - 2) * (S / a1[n]) / (6.0 * (n - 1))) +
+                                ((S * (S - 1) / ((a1[n] * a1[n]) + a2[n])) *
+                                 (18.0 * (n * n) * (3.0 * n + 2.0) * a2[n + 1] - (88.0 * n * n * n + 9.0 * (n * n) - 13.0 * n + 6.0)) /
+                                 (9.0 * n * ((n - 1) * (n - 1)))));
+        } else {
+            td[i] = std::numeric_limits<double>::quiet_NaN();
+            fwh[i] = std::numeric_limits<double>::quiet_NaN();
+        }
+    }
+    head(o, c, W);
+    for (int i = 0; i < np; i++) {
+        o.str("\tD[" + popname(c, i) + "]:\t");
+        if (std::isnan(td[i])) o.na(); else o.f(td[i]);
+        o.str("\tH[" + popname(c, i) + "]:\t");
+        if (std::isnan(fwh[i])) o.na(); else o.f(fwh[i]);
+    }
+    o.str("\n");
+}
+
+// ---- ld: calc_zns pop_ld.cpp:201-252, calc_omegamax 254-373, calc_wall 375-458, print_ld 650-712
+inline double r2_of(unsigned m1, unsigned m2, unsigned c11, int n) {
+    double x0 = (double)m1 / n, x1 = (double)m2 / n, x11 = (double)c11 / n;
+    return ((x11 - x0 * x1) * (x11 - x0 * x1)) / (x0 * (1. - x0) * x1 * (1. - x1));
+}
+
+void do_ld(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
+    int np = p->n_pops;
+    int S = W.segsites;
+    std::vector<int> num_snps(np, 0);
+    std::vector<double> val(np, 0.0), wallq(np, 0.0);
+    const int mf = c->min_freq;
+    auto var = [&](unsigned m, int i) { return (int)m >= mf && (int)m <= p->pop_n[i] - mf; };
+    if (c->output == 1) {  // omega max
+        if (S >= 1)
+            for (int j = 0; j < np; j++) {
+                std::vector<std::vector<double>> r2(S, std::vector<double>(S, 0.0));
+                num_snps[j] = 0;
+                int count1 = 0, count2 = 0;
+                for (int i = 0; i < S - 1; i++) {
+                    uint64_t t1 = W.types[W.idx[i]] & p->pop_mask[j];
+                    unsigned m1 = popcnt64(t1);
+                    if (var(m1, j)) {
+                        ++num_snps[j];
+                        count2 = count1;
+                        for (int k = i + 1; k < S; k++) {
+                            uint64_t t2 = W.types[W.idx[k]] & p->pop_mask[j];
+                            unsigned m2 = popcnt64(t2);
+                            if (var(m2, j)) {
+                                ++count2;
+                                r2[count1][count2] = r2_of(m1, m2, popcnt64(t1 & t2), p->pop_n[j]);
+                                r2[count2][count1] = r2[count1][count2];
+                            }
+                        }
+                        ++count1;
+                    }
+                }
+                ++num_snps[j];
+                double sl = 0, sr = 0, sb = 0;
+                val[j] = 0;
+                int ns = num_snps[j];
+                for (int i = 1; i < ns - 1; i++) {
+                    for (int k = 0; k < i; k++)
+                        for (int m = k + 1; m <= i; m++) sl += r2[k][m];
+                    for (int k = i + 1; k < ns; k++)
+                        for (int m = 0; m <= i; m++) sb += r2[k][m];
+                    for (int k = i + 1; k < ns - 1; k++)
+                        for (int m = k + 1; m < ns; m++) sr += r2[k][m];
+                    int left = i + 1, right = ns - left;
+                    double omega = (sl + sr) / (((left * (left - 1)) / 2.0) + ((right * (right - 1)) / 2.0));
+                    omega *= left * right / sb;
+                    val[j] = omega > val[j] ? omega : val[j];
+                }
+            }
+    } else if (c->output == 2) {  // Wall's B and Q
+        if (S >= 1) {
+            uint64_t last_type = 0;  // shared across populations (Appendix A.9)
+            std::vector<int> cong(np, 0), part(np, 0);
+            std::vector<std::vector<uint64_t>> uniq(np);
+            for (int i = 0; i < S; i++)
+                for (int j = 0; j < np; j++) {
+                    uint64_t t = W.types[W.idx[i]];
+                    uint64_t type = t & p->pop_mask[j];
+                    uint64_t comp = ~t & p->pop_mask[j];
+                    if (type > 0 && type < p->pop_mask[j]) {
+                        if (num_snps[j] == 0) {
+                            uniq[j].push_back(type);
+                            last_type = type;
+                            num_snps[j]++;
+                        } else {
+                            if (type == last_type || comp == last_type) {
+                                cong[j]++;
+                                long x = std::count(uniq[j].begin(), uniq[j].end(), type);
+                                long y = std::count(uniq[j].begin(), uniq[j].end(), comp);
+                                if (x == 0 && y == 0) {
+                                    uniq[j].push_back(type);
+                                    part[j]++;
+                                }
+                            }
+                            num_snps[j]++;
+                            last_type = type;
+                        }
+                    }
+                }
+            for (int i = 0; i < np; i++) {
+                val[i] = (double)cong[i] / (double)(num_snps[i] - 1);
+                wallq[i] = (double)(cong[i] + part[i]) / num_snps[i];
+            }
+        }
+    } else {  // ZnS
+        if (S >= 1)
+            for (int i = 0; i < np; i++) {
+                num_snps[i] = 0;
+                for (int j = 0; j < S - 1; j++) {
+                    uint64_t t1 = W.types[W.idx[j]] & p->pop_mask[i];
+                    unsigned m1 = popcnt64(t1);
+                    if (var(m1, i)) {
+                        ++num_snps[i];
+                        for (int k = j + 1; k < S; k++) {
+                            uint64_t t2 = W.types[W.idx[k]] & p->pop_mask[i];
+                            unsigned m2 = popcnt64(t2);
+                            if (var(m2, i)) val[i] += r2_of(m1, m2, popcnt64(t1 & t2), p->pop_n[i]);
+                        }
+                    }
+                }
+                ++num_snps[i];
+                val[i] *= 2.0 / (num_snps[i] * (num_snps[i] - 1));
+            }
+    }
+    head(o, c, W);
+    for (int i = 0; i < np; i++) {
+        o.str("\tS[" + popname(c, i) + "]:\t"); o.i(num_snps[i]);
+        bool ok = num_snps[i] >= c->min_snps;
+        if (c->output == 1) { o.str("\tomax[" + popname(c, i) + "]:\t"); if (ok) o.f(val[i]); else o.na(); }
+        else if (c->output == 2) {
+            o.str("\tB[" + popname(c, i) + "]:\t"); if (ok) o.f(val[i]); else o.na();
+            o.str("\tQ[" + popname(c, i) + "]:\t"); if (ok) o.f(wallq[i]); else o.na();
+        } else { o.str("\tZns[" + popname(c, i) + "]:\t"); if (ok) o.f(val[i]); else o.na(); }
+    }
+    o.str("\n");
+}
+
+// ---- diverge: calc_diverge pop_diverge.cpp:220-257, print_diverge 496-574
+void do_diverge(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
+    int n = p->n_samples, np = p->n_pops;
+    head(o, c, W);
+    bool ok = W.num_sites >= c->min_sites;
+    if (c->output == 0) {
+        int words = (W.segsites - 1) / 64;
+        for (int i = 0; i < n; i++) {
+            uint16_t d = 0;
+            for (int j = 0; j <= words; j++) d += (uint16_t)popcnt64(W.seq[i][j]);
+            o.str(std::string("\td[") + c->sample_names[i] + "]:\t");
+            if (!ok) { o.na(); continue; }
+            double pd = (double)d / W.num_sites;
+            o.f(c->jc ? -0.75 * std::log(1.0 - pd * (4.0 / 3.0)) : pd);
+        }
+    } else {
+        for (int i = 0; i < np; i++) {
+            int segs = 0;
+            uint16_t fixed = 0;
+            for (int j = 0; j < W.segsites; j++) {
+                uint64_t t = W.types[W.idx[j]];
+                uint64_t pt = t & p->pop_mask[i];
+                unsigned short freq;
+                if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(p->pop_n[i] - popcnt64(pt));
+                else freq = (unsigned short)popcnt64(pt);
+                if (freq > 0 && freq < p->pop_n[i]) ++segs;
+                else if (freq == p->pop_n[i]) ++fixed;
+            }
+            std::string pn = popname(c, i);
+            if (!ok) {
+                o.str("\tFixed[" + pn + "]:\t"); o.na(); o.str("\tSeg[" + pn + "]:\t"); o.na();
+                o.str("\td[" + pn + "]:\t"); o.na();
+                continue;
+            }
+            o.str("\tFixed[" + pn + "]:\t"); o.i(fixed);
+            o.str("\tSeg[" + pn + "]:\t"); o.i(segs);
+            o.str("\td[" + pn + "]:\t");
+            double pd = (p->flag & 0x10) ? (double)fixed / W.num_sites : (double)(fixed + segs) / W.num_sites;
+            o.f(c->jc ? -0.75 * std::log(1.0 - pd * (4.0 / 3.0)) : pd);
+        }
+    }
+    o.str("\n");
+}
+
+// ---- haplo: calc_nhaps pop_haplo.cpp:208-254, calc_ehhs 256-323, calc_minDxy 325-363,
+//             print_haplo 365-442
+void do_haplo(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
+    int n = p->n_samples, np = p->n_pops;
+    auto d = diff_matrix(p, W);
+    std::vector<int> nhaps(np, 0);
+    std::vector<double> hdiv(np, 0.0), ehhs(np, 0.0), piw(np, 0.0);
+    int npairs = np * (np - 1) > 0 ? np * (np - 1) : 1;
+    std::vector<double> pib(npairs, 0.0);
+    std::vector<uint16_t> minDxy(npairs, 0);
+    auto nhaps_fn = [&]() {
+        for (int i = 0; i < np; i++) {
+            int nelem = p->pop_n[i];
+            if (nelem > 1) {
+                std::vector<int> b;
+                for (int j = 0; j < n; j++)
+                    if (p->pop_mask[i] >> j & 1) b.push_back(j);
+                // local indices j,k index the GLOBAL diff matrix (Appendix A.11)
+                for (int j = 0; j < nelem - 1; j++)
+                    for (int k = j + 1; k < nelem; k++)
+                        if (d[j][k] == 0 && b[k] > b[j]) b.at(k) = j;
+                int ff = 0;
+                for (int j = 0; j < (int)b.size(); j++) {
+                    int f = (int)std::count(b.begin(), b.end(), j);
+                    if (f > 0) ++nhaps[i];
+                    ff += f * f;
+                }
+                double sh = (double)(ff) / (double)(nelem * nelem);
+                hdiv[i] = 1.0 - ((1.0 - sh) * (double)(nelem / (nelem - 1)));
+            } else {
+                nhaps[i] = 1;
+                hdiv[i] = 1.0;
+            }
+        }
+    };
+    if (c->output == 0) nhaps_fn();
+    else if (c->output == 1) {
+        nhaps_fn();
+        for (int i = 0; i < np; i++) {
+            if (p->pop_n[i] < 4) { ehhs[i] = std::numeric_limits<double>::quiet_NaN(); continue; }
+            std::list<uint64_t> pop_site;
+            for (int j = 0; j < W.segsites; j++) {
+                uint64_t pt = W.types[W.idx[j]] & p->pop_mask[i];
+                unsigned short popf = (unsigned short)popcnt64(pt);
+                if (popf > 1 && popf < p->pop_n[i] - 1) pop_site.push_back(pt);
+            }
+            int part_max_count = 0;
+            uint64_t comp = 0, max_site = 0;
+            std::list<uint64_t> uniq(pop_site);
+            uniq.sort();
+            uniq.unique();
+            for (uint64_t pt : uniq) {
+                // ~CHECK_BIT(...) is always non-zero: comp accumulates pop_mask (A.11)
+                for (int j = 0; j < n; j++)
+                    if (p->pop_mask[i] >> j & 1) comp |= 0x1ULL << j;
+                int before = (int)pop_site.size();
+                pop_site.remove(pt);
+                pop_site.remove(comp);
+                int after = (int)pop_site.size();
+                int part_count = (before - after) + 1;
+                if (part_count > part_max_count) { part_max_count = part_count; max_site = pt; }
+            }
+            unsigned short popf = (unsigned short)popcnt64(max_site);
+            int pn = p->pop_n[i];
+            double sh = (1.0 - ((double)((popf * popf) + ((pn - popf) * (pn - popf))) / (pn * pn))) * (double)(pn / (pn - 1));
+            ehhs[i] = hdiv[i] / (1.0 - sh);
+        }
+    } else {
+        for (int i = 0; i < np; i++)
+            for (int j = i; j < np; j++) {
+                int pi = i * np + (j - (i + 1));
+                if (i != j) minDxy[pi] = (uint16_t)0xFFFFFFFFu;  // UINT_MAX into u16 (A.7)
+                for (int v = 0; v < n - 1; v++)
+                    for (int w = v + 1; w < n; w++)
+                        if ((p->pop_mask[i] >> v & 1) && (p->pop_mask[j] >> w & 1)) {
+                            if (i == j) piw[i] += (double)d[v][w];
+                            else {
+                                pib[pi] += (double)d[v][w];
+                                minDxy[pi] = minDxy[pi] < d[v][w] ? minDxy[pi] : d[v][w];
+                            }
+                        }
+                if (i != j) pib[pi] *= 1.0 / (double)(p->pop_n[i] * p->pop_n[j]);
+                else {
+                    piw[i] *= 2.0 / (double)(p->pop_n[i] * (p->pop_n[i] - 1));
+                    if (std::isnan(piw[i])) piw[i] = 0.0;
+                }
+            }
+    }
+    head(o, c, W);
+    bool ok = W.num_sites >= c->min_sites;
+    if (c->output == 0) {
+        for (int i = 0; i < np; i++) {
+            std::string pn = popname(c, i);
+            if (ok) { o.str("\tK[" + pn + "]:\t"); o.i(nhaps[i]); o.str("\tKdiv[" + pn + "]:\t"); o.f(1.0 - hdiv[i]); }
+            else { o.str("\tK[" + pn + "]:\t"); o.na(); o.str("\tKdiv[" + pn + "]:\t"); o.na(); }
+        }
+    } else if (c->output == 1) {
+        for (int i = 0; i < np; i++) {
+            o.str("\tEHHS[" + popname(c, i) + "]:\t");
+            if (ok && !std::isnan(ehhs[i])) o.f(ehhs[i]); else o.na();
+        }
+    } else {
+        for (int i = 0; i < np; i++) { o.str("\tpi[" + popname(c, i) + "]:\t"); if (ok) o.f(piw[i]); else o.na(); }
+        for (int i = 0; i < np - 1; i++)
+            for (int j = i + 1; j < np; j++) {
+                std::string pp = popname(c, i) + "-" + popname(c, j);
+                int pi = i * np + (j - (i + 1));
+                if (ok) { o.str("\tdxy[" + pp + "]:\t"); o.f(pib[pi]); o.str("\tmin[" + pp + "]:\t"); o.i(minDxy[pi]); }
+                else { o.str("\tdxy[" + pp + "]:\t"); o.na(); o.str("\tmin[" + pp + "]:\t"); o.na(); }
+            }
+    }
+    o.str("\n");
+}
+
+// ---- snp -o 0: print_popbam_snp pop_snp.cpp:224-241.  A genotype byte >= 16 (segbase
+// borrow) makes the reference read iupac[] out of bounds (UB); we print '?' there and the
+// tests mask that column.
+void do_snp(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
+    for (int i = 0; i < W.segsites; i++) {
+        o.str(c->chr_name); o.str("\t"); o.i((long long)W.pos[i] + 1); o.str("\t");
+        char rc[2] = {nt16_char((unsigned char)W.refc[i]), 0};
+        o.str(rc);
+        for (int j = 0; j < p->n_samples; j++) {
+            unsigned char g = W.gbyte[j][i];
+            char bc[2] = {g < 16 ? nt16_char((unsigned char)kIupac[g]) : '?', 0};
+            o.str("\t"); o.str(bc);
+            o.str("\t"); o.i(W.snpq[j][i]);
+            o.str("\t"); o.i(W.rms[j][i]);
+            o.str("\t"); o.i(W.nreads[j][i]);
+        }
+        o.str("\n");
+    }
+}
+
+struct SiteResult {
+    std::vector<uint64_t> cb, types;
+    std::vector<int16_t> fq;
+    std::vector<uint8_t> flags;
+};
+
+void call_range(const orc_params *p, uint32_t n_sites, const uint8_t *ref, const uint16_t *depth,
+                const uint32_t *reads, uint64_t *cb, uint64_t *types, int16_t *fq, uint8_t *flags) {
+    const int n = p->n_samples;
+    std::vector<uint64_t> tmp(n);
+    size_t off = 0;
+    for (uint32_t s = 0; s < n_sites; s++) {
+        const uint16_t *dp = depth + (size_t)s * n;
+        uint64_t *c = cb ? cb + (size_t)s * n : tmp.data();
+        size_t tot = 0;
+        for (int j = 0; j < n; j++) tot += dp[j];
+        uint8_t fl = 0;
+        uint64_t ty = 0;
+        int f = 0;
+        if (!(ref[s] & 0x80)) {  // make_<cmd> only runs for positions the pileup called back
+            fl |= 1;
+            call_base(p, dp, reads + off, c);
+            char rch = (char)ref[s];
+            if (!(p->flag & 0x20)) clean_heterozygotes(n, c, (int)rch, p->min_snpQ);
+            f = segbase(n, c, rch, p->min_snpQ);
+            uint64_t cov = qfilter(n, c, p->min_rmsQ, p->min_depth, p->max_depth);
+            if ((int)popcnt64(cov) == n) {
+                fl |= 2;
+                for (int i = 0; i < n; i++)
+                    if ((c[i] & 3ULL) == 3ULL) ty |= 1ULL << i;
+                if (f > 0) fl |= 4;
+            }
+        } else if (cb) {
+            for (int j = 0; j < n; j++) c[j] = 0;
+        }
+        off += tot;
+        if (types) types[s] = ty;
+        if (fq) fq[s] = (int16_t)f;
+        if (flags) flags[s] = fl;
+    }
+}
+
+void add_site(Window &W, const orc_params *p, uint32_t pos, uint64_t ty, uint8_t fl, const uint64_t *cb, char refc) {
+    if (!(fl & 2)) return;
+    int n = p->n_samples;
+    W.types.push_back(ty);
+    if (fl & 4) {
+        int s = W.segsites;
+        for (int i = 0; i < n; i++) {
+            if ((size_t)(s / 64) >= W.seq[i].size()) W.seq[i].push_back(0);
+            if (ty >> i & 1) W.seq[i][s / 64] |= 0x1ULL << (s % 64);
+            if (cb) {
+                W.snpq[i].push_back((cb[i] >> 32) & 0xffff);
+                W.rms[i].push_back((cb[i] >> 48) & 0xffff);
+                W.nreads[i].push_back((cb[i] >> 16) & 0xffff);
+                W.gbyte[i].push_back((cb[i] >> 8) & 0xff);
+            }
+        }
+        W.idx.push_back(W.num_sites);
+        W.pos.push_back(pos);
+        W.refc.push_back(refc);
+        W.segsites++;
+    }
+    W.num_sites++;
+}
+
+void init_window(Window &W, const orc_params *p, int b, int e) {
+    int n = p->n_samples;
+    W = Window();
+    W.beg = b; W.end = e;
+    W.seq.assign(n, std::vector<uint64_t>(1, 0));
+    W.snpq.assign(n, {}); W.rms.assign(n, {}); W.nreads.assign(n, {}); W.gbyte.assign(n, {});
+}
+
+void emit(Out &o, const orc_params *p, const orc_cmd *c, const Window &W, const SfsConst &K) {
+    switch (c->cmd) {
+        case ORC_NUCDIV: do_nucdiv(o, p, c, W); break;
+        case ORC_SFS: do_sfs(o, p, c, W, K); break;
+        case ORC_LD: do_ld(o, p, c, W); break;
+        case ORC_DIVERGE: do_diverge(o, p, c, W); break;
+        case ORC_HAPLO: do_haplo(o, p, c, W); break;
+        case ORC_SNP: do_snp(o, p, c, W); break;
+        default: break;
+    }
+}
+
+long finish(const Out &o, char *out, size_t cap) {
+    if (o.s.size() + 1 > cap) return -(long)(o.s.size() + 1);
+    std::memcpy(out, o.s.c_str(), o.s.size() + 1);
+    return (long)o.s.size();
+}
+
+}  // namespace
+
+extern "C" {
+
+const double *orc_fk(void) { return tables().fk.data(); }
+const double *orc_beta(void) { return tables().beta.data(); }
+const double *orc_lhet(void) { return tables().lhet.data(); }
+
+int orc_call_sites(const orc_params *p, uint32_t n_sites, const uint8_t *ref, const uint16_t *depth,
+                   const uint32_t *reads, uint64_t *cb, uint64_t *types, int16_t *fq, uint8_t *flags) {
+    if (!p || p->n_samples < 1 || p->n_samples > 64) return -1;
+    call_range(p, n_sites, ref, depth, reads, cb, types, fq, flags);
+    return 0;
+}
+
+// main_<cmd> window loop, e.g. pop_nucdiv.cpp:47-124
+long orc_run(const orc_params *p, const orc_cmd *c, uint32_t n_sites, const uint8_t *ref,
+             const uint16_t *depth, const uint32_t *reads, char *out, size_t cap) {
+    if (!p || !c || p->n_samples < 1 || p->n_samples > 64) return -1;
+    const int n = p->n_samples;
+    int beg = c->beg, end = c->end;
+    if (end > (int)n_sites) end = (int)n_sites;
+    // per-site calls over [beg, end) (each window's re-fetch yields the same pileup per site)
+    size_t off = 0;
+    for (int s = 0; s < beg; s++)
+        for (int j = 0; j < n; j++) off += depth[(size_t)s * n + j];
+    int len = end > beg ? end - beg : 0;
+    std::vector<uint64_t> cb((size_t)len * n), types(len);
+    std::vector<int16_t> fq(len);
+    std::vector<uint8_t> flags(len);
+    if (len) call_range(p, (uint32_t)len, ref + beg, depth + (size_t)beg * n, reads + off, cb.data(), types.data(), fq.data(), flags.data());
+    long num_windows;
+    long long w = c->win_size;
+    if (c->windowed) num_windows = ((c->end - c->beg) - 1) / w;
+    else { w = c->end - c->beg; num_windows = 1; }
+    SfsConst K = sfs_const(n);
+    Out o;
+    Window W;
+    for (long cw = 0; cw < num_windows; cw++) {
+        int wb, we;
+        if (c->windowed) {  // "chr:beg+cw*w+1-(cw+1)*w+beg-1" through bam_parse_region
+            wb = (int)(c->beg + cw * w);
+            we = (int)((cw + 1) * w + (c->beg - 1));
+        } else { wb = c->beg; we = c->end; }
+        init_window(W, p, wb, we);
+        for (int pos = wb; pos < we && pos < end; pos++) {
+            if (pos < beg) continue;
+            int s = pos - beg;
+            add_site(W, p, (uint32_t)pos, types[s], flags[s], cb.data() + (size_t)s * n, (char)ref[pos]);
+        }
+        emit(o, p, c, W, K);
+    }
+    return finish(o, out, cap);
+}
+
+long orc_windows_from_sites(const orc_params *p, const orc_cmd *c, const uint64_t *types,
+                            const uint8_t *flags, uint32_t n_win, const int32_t *wbeg,
+                            const int32_t *wend, char *out, size_t cap) {
+    if (!p || !c) return -1;
+    SfsConst K = sfs_const(p->n_samples);
+    Out o;
+    Window W;
+    for (uint32_t i = 0; i < n_win; i++) {
+        init_window(W, p, wbeg[i], wend[i]);
+        for (int pos = wbeg[i]; pos < wend[i]; pos++) add_site(W, p, (uint32_t)pos, types[pos], flags[pos], nullptr, 0);
+        emit(o, p, c, W, K);
+    }
+    return finish(o, out, cap);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- synthetic pileup
+// Test-only restatement of the benchmark generator (popbam_amd/csrc/pbg_common.h), so CPU
+// parity checks can regenerate any position of the HBM-resident workload.
+namespace {
+uint64_t sm64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+}  // namespace
+
+extern "C" void orc_synth_site(uint64_t seed, uint64_t pos, int32_t n, int32_t mean_depth, uint8_t *ref,
+                               uint16_t *depth, uint32_t *reads, uint32_t *n_reads_out) {
+    uint64_t h = sm64(seed ^ sm64(pos));
+    int ref_idx = (int)(h & 3);
+    int snp = ((h >> 2) & 0x3FF) < 12;
+    int alt = (ref_idx + 1 + (int)((h >> 12) % 3)) & 3;
+    uint32_t f16 = (uint32_t)((h >> 16) & 0xFFFF);
+    *ref = (uint8_t)"ACGT"[ref_idx];
+    uint32_t nr = 0;
+    for (int s = 0; s < n; ++s) {
+        uint64_t hs = sm64(h ^ (0xD1B54A32D192ED03ULL * (uint64_t)(s + 1)));
+        uint64_t bits = sm64(hs ^ 0x5851F42D4C957F2DULL);
+        int nb = 2 * mean_depth;
+        uint64_t m = nb >= 64 ? ~0ULL : ((1ULL << nb) - 1);
+        int d = __builtin_popcountll(bits & m);
+        depth[s] = (uint16_t)d;
+        int a0 = (snp && (uint32_t)(hs & 0xFFFF) < f16) ? alt : ref_idx;
+        int a1 = (snp && (uint32_t)((hs >> 16) & 0xFFFF) < f16) ? alt : ref_idx;
+        for (int r = 0; r < d; ++r) {
+            uint64_t hr = sm64(hs + (uint64_t)r + 1);
+            int base = (hr & 1) ? a1 : a0;
+            if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((hr >> 8) % 3)) & 3;
+            uint32_t bq = 20 + (uint32_t)((hr >> 16) % 21);
+            uint32_t strand = (uint32_t)((hr >> 40) & 1);
+            if (reads) reads[nr] = bq | (60u << 8) | ((1u << base) << 16) | (strand << 20);
+            ++nr;
+        }
+    }
+    *n_reads_out = nr;
+}

@@ -1,0 +1,136 @@
+"""ctypes binding of libpopbam_gpu.so (include/popbam_gpu.h).
+
+The library is built in-tree by popbam_amd/csrc/Makefile (`python -c "import
+__graft_entry__ as g; g.build()"`).  There is no CPU fallback: `load()` raises if the
+shared object is missing, and every compute entry point fails with PBG_E_NODEV when no
+HIP device is visible.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpopbam_gpu.so")
+
+PBG_MAX_SAMPLES = 64
+PBG_MAX_POPS = 16
+PBG_SITE_BLOCK = 64
+
+PBG_OK, PBG_E_ARG, PBG_E_HIP, PBG_E_NOMEM, PBG_E_RANGE, PBG_E_NODEV = 0, -1, -2, -3, -4, -5
+
+PBG_S_NUCDIV, PBG_S_SFS, PBG_S_ZNS, PBG_S_OMEGA, PBG_S_WALL = 0x1, 0x2, 0x4, 0x8, 0x10
+PBG_S_DIV_IND, PBG_S_DIV_POP, PBG_S_HAP_K, PBG_S_HAP_EHHS, PBG_S_HAP_DXY = 0x20, 0x40, 0x80, 0x100, 0x200
+
+# every symbol include/popbam_gpu.h declares
+EXPORTS = ["pbg_create", "pbg_destroy", "pbg_last_error", "pbg_row_bytes", "pbg_device_count",
+           "pbg_call_sites", "pbg_window_stats", "pbg_run", "pbg_format", "pbg_synth_depth", "pbg_synth_reads"]
+
+
+class PbgParams(C.Structure):
+    _fields_ = [("n_samples", C.c_int32), ("n_pops", C.c_int32), ("pop_mask", C.c_uint64 * PBG_MAX_POPS),
+                ("pop_n", C.c_int32 * PBG_MAX_POPS), ("min_depth", C.c_int32), ("max_depth", C.c_int32),
+                ("min_rmsQ", C.c_int32), ("min_snpQ", C.c_int32), ("min_mapQ", C.c_int32),
+                ("min_baseQ", C.c_int32), ("flag", C.c_uint32)]
+
+
+class PbgPileup(C.Structure):
+    _fields_ = [("n_sites", C.c_uint32), ("pos0", C.c_int32), ("ref", C.c_void_p), ("depth", C.c_void_p),
+                ("block_off", C.c_void_p), ("reads", C.c_void_p)]
+
+
+class PbgWindow(C.Structure):
+    _fields_ = [("beg", C.c_int32), ("end", C.c_int32)]
+
+
+class PbgStatOpts(C.Structure):
+    _fields_ = [("stats", C.c_uint32), ("min_freq", C.c_int32), ("outidx", C.c_int32), ("jc", C.c_int32)]
+
+
+class PbgWindowOut(C.Structure):
+    _fields_ = [(nm, C.c_void_p) for nm in
+                ("num_sites", "segsites", "pi", "dxy", "td", "fwh", "ld_snps", "ld_val", "ld_q", "div_ind",
+                 "div_fixed", "div_seg", "div_pop", "nhaps", "hap_val", "hap_dxy", "hap_min")]
+
+
+class PbgCmd(C.Structure):
+    _fields_ = [("cmd", C.c_int32), ("output", C.c_int32), ("min_sites", C.c_int32), ("min_snps", C.c_int32),
+                ("min_freq", C.c_int32), ("outidx", C.c_int32), ("jc", C.c_int32), ("windowed", C.c_int32),
+                ("win_size", C.c_int64), ("beg", C.c_int32), ("end", C.c_int32), ("chr_name", C.c_char_p),
+                ("sample_names", C.POINTER(C.c_char_p)), ("pop_names", C.POINTER(C.c_char_p))]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                           "(there is no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    vp = C.c_void_p
+    lib.pbg_create.argtypes = [P(vp), C.c_int, P(PbgParams)]
+    lib.pbg_create.restype = C.c_int
+    lib.pbg_destroy.argtypes = [vp]
+    lib.pbg_destroy.restype = None
+    lib.pbg_last_error.argtypes = [vp]
+    lib.pbg_last_error.restype = C.c_char_p
+    lib.pbg_row_bytes.argtypes = [vp]
+    lib.pbg_row_bytes.restype = C.c_int
+    lib.pbg_device_count.argtypes = []
+    lib.pbg_device_count.restype = C.c_int
+    lib.pbg_call_sites.argtypes = [vp, P(PbgPileup), vp, vp, vp]
+    lib.pbg_call_sites.restype = C.c_int
+    lib.pbg_window_stats.argtypes = [vp, vp, C.c_uint32, vp, C.c_uint32, P(PbgStatOpts), P(PbgWindowOut), vp]
+    lib.pbg_window_stats.restype = C.c_int
+    lib.pbg_run.argtypes = [vp, P(PbgCmd), P(PbgPileup), C.c_char_p, C.c_size_t, P(C.c_size_t)]
+    lib.pbg_run.restype = C.c_long
+    lib.pbg_format.argtypes = [vp, P(PbgCmd), P(PbgWindowOut), C.c_uint32, vp, vp, C.c_char_p, C.c_size_t,
+                               P(C.c_size_t)]
+    lib.pbg_format.restype = C.c_long
+    lib.pbg_synth_depth.argtypes = [vp, C.c_uint64, C.c_int32, C.c_uint32, vp, vp, vp, P(C.c_uint64), vp]
+    lib.pbg_synth_depth.restype = C.c_int
+    lib.pbg_synth_reads.argtypes = [vp, C.c_uint64, C.c_int32, C.c_uint32, vp, vp, vp, vp]
+    lib.pbg_synth_reads.restype = C.c_int
+    _lib = lib
+    return lib
+
+
+class PbgError(RuntimeError):
+    pass
+
+
+class Context:
+    """Owns one pbg_ctx (one device)."""
+
+    def __init__(self, params: PbgParams, device: int = 0):
+        self.lib = load()
+        self.h = C.c_void_p()
+        rc = self.lib.pbg_create(C.byref(self.h), device, C.byref(params))
+        if rc != PBG_OK:
+            raise PbgError(f"pbg_create failed ({rc}): {self.lib.pbg_last_error(None).decode()}")
+        self.params = params
+
+    def check(self, rc, what):
+        if rc < 0:
+            raise PbgError(f"{what} failed ({rc}): {self.lib.pbg_last_error(self.h).decode()}")
+        return rc
+
+    @property
+    def row_bytes(self):
+        return self.lib.pbg_row_bytes(self.h)
+
+    def close(self):
+        if self.h:
+            self.lib.pbg_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

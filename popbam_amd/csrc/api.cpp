@@ -1,0 +1,534 @@
+// api.cpp -- the C-ABI of include/popbam_gpu.h: context, launches and `pbg_run`.
+//
+// pbg_run restates the window loop of main_<cmd> (e.g. pop_nucdiv.cpp:47-124): windows of
+// `win_size` bases [beg + cw*w, beg + (cw+1)*w - 1) (the last base is dropped, Appendix A.1),
+// num_windows = ((end-beg)-1)/w, or the whole region without -w.  Unlike the reference,
+// which re-fetches and re-piles reads for every window, all positions of the region are
+// called in one launch and every window is reduced in one launch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "pbg_common.h"
+#include "pbg_host.h"
+
+struct pbg_ctx {
+    int device = 0;
+    pbg_params params{};
+    pbg::DevParams dp{};
+    pbg::DevTables dt{};
+    int row_bytes = 8;
+    double *d_fk = nullptr, *d_beta = nullptr, *d_lhet = nullptr, *d_sfs = nullptr, *d_r2 = nullptr;
+    int *d_err = nullptr;
+    std::string err;
+    // per-pileup LDS staging capacity (keyed by block_off pointer and size), so repeated
+    // calls on the same resident batch do not synchronise
+    const void *cap_key = nullptr;
+    uint32_t cap_sites = 0, cap_val = 0;
+    // per-window-list workspace plan (keyed by the device window array)
+    const void *ws_key = nullptr;
+    uint32_t ws_nwin = 0, ws_nrows = 0, ws_stats = 0;
+    bool ws_need = false;
+    uint64_t *d_ws = nullptr, *d_wsoff = nullptr;
+    size_t ws_cap = 0, wsoff_cap = 0;
+};
+
+namespace {
+
+thread_local std::string g_create_error;
+
+int fail(pbg_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    else g_create_error = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                          \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess)                                                                      \
+            return fail((ctx), PBG_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+    } while (0)
+
+int row_bytes_for(int n) { return n <= 14 ? 2 : n <= 30 ? 4 : n <= 62 ? 8 : 16; }
+
+template <class T>
+hipError_t upload(T **dst, const std::vector<T> &v) {
+    hipError_t e = hipMalloc((void **)dst, std::max<size_t>(1, v.size()) * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (v.empty()) return hipSuccess;
+    return hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+struct DevBuf {   // RAII device allocation for pbg_run
+    void *p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t bytes) { return hipMalloc(&p, std::max<size_t>(bytes, 16)); }
+};
+
+}  // namespace
+
+extern "C" {
+
+int pbg_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *pbg_last_error(const pbg_ctx *ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int pbg_row_bytes(const pbg_ctx *ctx) { return ctx ? ctx->row_bytes : 0; }
+
+int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
+    if (!out || !p) return fail(nullptr, PBG_E_ARG, "null argument");
+    *out = nullptr;
+    if (p->n_samples < 1 || p->n_samples > PBG_MAX_SAMPLES)
+        return fail(nullptr, PBG_E_ARG, "n_samples must be in [1, 64] (u64 sample masks, popbam.1:507-510)");
+    if (p->n_pops < 1 || p->n_pops > PBG_MAX_POPS) return fail(nullptr, PBG_E_ARG, "n_pops must be in [1, 16]");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(nullptr, PBG_E_NODEV, "no HIP device visible (libpopbam_gpu has no CPU path)");
+    if (device < 0 || device >= ndev) return fail(nullptr, PBG_E_NODEV, "device index out of range");
+    pbg_ctx *c = new pbg_ctx();
+    c->device = device;
+    c->params = *p;
+    c->row_bytes = row_bytes_for(p->n_samples);
+    pbg::DevParams &d = c->dp;
+    d.n = p->n_samples;
+    d.npops = p->n_pops;
+    for (int i = 0; i < PBG_MAX_POPS; ++i) {
+        d.pop_mask[i] = i < p->n_pops ? p->pop_mask[i] : 0;
+        d.pop_n[i] = i < p->n_pops ? p->pop_n[i] : 0;
+    }
+    d.min_depth = p->min_depth;
+    d.max_depth = p->max_depth;
+    d.min_rmsQ = p->min_rmsQ;
+    d.min_snpQ = p->min_snpQ;
+    d.min_mapQ = p->min_mapQ & 0xff;
+    d.min_baseQ = p->min_baseQ & 0xff;
+    d.flag = p->flag;
+    auto bad = [&](hipError_t e, const char *what) {
+        std::string m = std::string(what) + ": " + hipGetErrorString(e);
+        pbg_destroy(c);
+        return fail(nullptr, PBG_E_HIP, m);
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return bad(e, "hipSetDevice");
+    std::vector<double> fk, beta, lhet;
+    pbg::build_errmod_tables(fk, beta, lhet);
+    if ((e = upload(&c->d_fk, fk)) != hipSuccess) return bad(e, "upload fk");
+    if ((e = upload(&c->d_beta, beta)) != hipSuccess) return bad(e, "upload beta");
+    if ((e = upload(&c->d_lhet, lhet)) != hipSuccess) return bad(e, "upload lhet");
+    // Tajima constants are indexed by population size and built for n = sm->n (pop_sfs.cpp:53-56)
+    std::vector<double> a1, a2, e1, e2;
+    pbg::build_sfs_constants(p->n_samples, a1, a2, e1, e2);
+    const size_t L = a2.size();
+    std::vector<double> sfs(4 * L, 0.0);
+    std::copy(a1.begin(), a1.end(), sfs.begin());
+    std::copy(a2.begin(), a2.end(), sfs.begin() + L);
+    std::copy(e1.begin(), e1.end(), sfs.begin() + 2 * L);
+    std::copy(e2.begin(), e2.end(), sfs.begin() + 3 * L);
+    if ((e = upload(&c->d_sfs, sfs)) != hipSuccess) return bad(e, "upload sfs constants");
+    std::vector<double> r2all;
+    for (int i = 0; i < p->n_pops; ++i) {
+        std::vector<double> t;
+        pbg::build_r2_table(std::max(1, p->pop_n[i]), t);
+        c->dt.r2_off[i] = (int32_t)r2all.size();
+        r2all.insert(r2all.end(), t.begin(), t.end());
+    }
+    if ((e = upload(&c->d_r2, r2all)) != hipSuccess) return bad(e, "upload r2 tables");
+    if ((e = hipMalloc(&c->d_err, sizeof(int))) != hipSuccess) return bad(e, "hipMalloc err");
+    if ((e = hipMemset(c->d_err, 0, sizeof(int))) != hipSuccess) return bad(e, "hipMemset err");
+    c->dt.fk = c->d_fk;
+    c->dt.beta = c->d_beta;
+    c->dt.lhet = c->d_lhet;
+    c->dt.a1 = c->d_sfs;
+    c->dt.a2 = c->d_sfs + L;
+    c->dt.e1 = c->d_sfs + 2 * L;
+    c->dt.e2 = c->d_sfs + 3 * L;
+    c->dt.r2 = c->d_r2;
+    *out = c;
+    return PBG_OK;
+}
+
+void pbg_destroy(pbg_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
+                    (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff})
+        if (p) (void)hipFree(p);
+    delete c;
+}
+
+int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, void *stream) {
+    if (!c || !pl || !rows) return fail(c, PBG_E_ARG, "null argument");
+    if (pl->n_sites == 0) return PBG_OK;
+    if (!pl->ref || !pl->depth || !pl->block_off || !pl->reads) return fail(c, PBG_E_ARG, "null pileup array");
+    HIPCHK(c, hipSetDevice(c->device));
+    // LDS staging capacity: the mean block plus six standard deviations (Poisson-like),
+    // bounded by what one CU can give a workgroup; blocks above it read HBM directly
+    const uint32_t nblk = (pl->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
+    if (c->cap_key != (const void *)pl->block_off || c->cap_sites != pl->n_sites) {
+        uint64_t total = 0;
+        HIPCHK(c, hipMemcpyAsync(&total, pl->block_off + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                 (hipStream_t)stream));
+        HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+        const double mean = (double)total / nblk;
+        uint32_t cap = (uint32_t)(mean + 6.0 * std::sqrt(mean) + 64.0);
+        cap = (cap + 63) & ~63u;
+        const uint32_t max_cap = (uint32_t)((64 * 1024 - pbg::call_sites_lds_bytes(c->dp.n, 0)) / 4);
+        c->cap_val = std::min(std::max(cap, 256u), max_cap);
+        c->cap_key = pl->block_off;
+        c->cap_sites = pl->n_sites;
+    }
+    const uint32_t cap = c->cap_val;
+    HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, pl->n_sites, pl->ref, pl->depth, pl->block_off,
+                                     pl->reads, cap, rows, cb, c->d_err, (hipStream_t)stream));
+    return PBG_OK;
+}
+
+int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_window *wins, uint32_t n_win,
+                     const pbg_stat_opts *o, const pbg_window_out *out, void *stream) {
+    if (!c || !rows || !wins || !o || !out) return fail(c, PBG_E_ARG, "null argument");
+    if (n_win == 0) return PBG_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    pbg::StatsArgs A{};
+    A.stats = o->stats;
+    A.min_freq = o->min_freq;
+    A.outidx = o->outidx;
+    A.jc = o->jc;
+    A.wins = wins;
+    A.out = *out;
+    // global workspace: only for windows that outgrow LDS and for omega / Wall lists.  The
+    // plan is cached per device window list, so steady-state calls do not synchronise.
+    if (c->ws_key != (const void *)wins || c->ws_nwin != n_win || c->ws_nrows != n_rows || c->ws_stats != o->stats) {
+        std::vector<pbg_window> hw(n_win);
+        HIPCHK(c, hipMemcpyAsync(hw.data(), wins, n_win * sizeof(pbg_window), hipMemcpyDeviceToHost,
+                                 (hipStream_t)stream));
+        HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+        int64_t maxlen = 0;
+        std::vector<uint64_t> off(n_win);
+        uint64_t tot = 0;
+        for (uint32_t i = 0; i < n_win; ++i) {
+            if (hw[i].beg < 0 || hw[i].end < hw[i].beg || (uint32_t)hw[i].end > n_rows)
+                return fail(c, PBG_E_RANGE, "window outside the row range");
+            int64_t len = hw[i].end - hw[i].beg;
+            maxlen = std::max(maxlen, len);
+            off[i] = tot;
+            tot += pbg::ws_slice(len, c->dp.n, c->dp.npops);
+        }
+        c->ws_need = (o->stats & (PBG_S_OMEGA | PBG_S_WALL)) || maxlen > pbg::kSegCap ||
+                     (int64_t)c->dp.n * (maxlen / 64 + 1) > pbg::kPlaneCap;
+        if (c->ws_need) {
+            if (tot * 8 > c->ws_cap) {
+                if (c->d_ws) HIPCHK(c, hipFree(c->d_ws));
+                c->d_ws = nullptr;
+                HIPCHK(c, hipMalloc(&c->d_ws, tot * 8));
+                c->ws_cap = tot * 8;
+            }
+            if (n_win * 8 > c->wsoff_cap) {
+                if (c->d_wsoff) HIPCHK(c, hipFree(c->d_wsoff));
+                c->d_wsoff = nullptr;
+                HIPCHK(c, hipMalloc(&c->d_wsoff, n_win * 8));
+                c->wsoff_cap = n_win * 8;
+            }
+            HIPCHK(c, hipMemcpyAsync(c->d_wsoff, off.data(), n_win * 8, hipMemcpyHostToDevice, (hipStream_t)stream));
+            HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+        }
+        c->ws_key = wins;
+        c->ws_nwin = n_win;
+        c->ws_nrows = n_rows;
+        c->ws_stats = o->stats;
+    }
+    if (c->ws_need) {
+        A.ws = c->d_ws;
+        A.ws_off = c->d_wsoff;
+    }
+    HIPCHK(c, pbg::launch_window_stats(c->row_bytes, c->dp, c->dt, rows, n_rows, n_win, A, (hipStream_t)stream));
+    return PBG_OK;
+}
+
+int pbg_synth_depth(pbg_ctx *c, uint64_t seed, int32_t mean_depth, uint32_t n_sites, uint8_t *ref, uint16_t *depth,
+                    uint64_t *block_off, uint64_t *n_reads, void *stream) {
+    if (!c || !ref || !depth || !block_off) return fail(c, PBG_E_ARG, "null argument");
+    if (mean_depth < 1 || mean_depth > 32) return fail(c, PBG_E_ARG, "mean_depth must be in [1, 32]");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t nblk = (n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
+    HIPCHK(c, pbg::launch_synth_depth(seed, mean_depth, c->dp.n, n_sites, ref, depth, block_off, s));
+    // exclusive scan of the per-block totals on the host (one-off generation step)
+    std::vector<uint64_t> t(nblk + 1, 0);
+    HIPCHK(c, hipMemcpyAsync(t.data(), block_off, nblk * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    uint64_t run = 0;
+    for (uint32_t i = 0; i < nblk; ++i) {
+        uint64_t v = t[i];
+        t[i] = run;
+        run += v;
+    }
+    t[nblk] = run;
+    HIPCHK(c, hipMemcpyAsync(block_off, t.data(), (nblk + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (n_reads) *n_reads = run;
+    return PBG_OK;
+}
+
+int pbg_synth_reads(pbg_ctx *c, uint64_t seed, int32_t mean_depth, uint32_t n_sites, const uint16_t *depth,
+                    const uint64_t *block_off, uint32_t *reads, void *stream) {
+    if (!c || !depth || !block_off || !reads) return fail(c, PBG_E_ARG, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, pbg::launch_synth_reads(seed, mean_depth, c->dp.n, n_sites, depth, block_off, reads,
+                                      (hipStream_t)stream));
+    return PBG_OK;
+}
+
+long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, size_t cap, size_t *needed) {
+    if (!c || !cmd || !hp || (!out && cap)) return fail(c, PBG_E_ARG, "null argument");
+    if (hp->n_sites && (!hp->ref || !hp->depth || !hp->reads)) return fail(c, PBG_E_ARG, "null pileup array");
+    HIPCHK(c, hipSetDevice(c->device));
+    c->cap_key = nullptr;   // this call's buffers are fresh allocations: drop cached plans
+    c->ws_key = nullptr;
+    const int n = c->dp.n, np = c->dp.npops;
+    // ---- windows in contig coordinates (main_<cmd>)
+    std::vector<std::pair<int32_t, int32_t>> win;
+    if (cmd->windowed) {
+        const int64_t w = cmd->win_size;
+        if (w <= 0) return fail(c, PBG_E_ARG, "window size must be positive");
+        const int64_t nw = ((int64_t)(cmd->end - cmd->beg) - 1) / w;
+        for (int64_t cw = 0; cw < nw; ++cw)
+            win.emplace_back((int32_t)(cmd->beg + cw * w), (int32_t)((cw + 1) * w + (cmd->beg - 1)));
+    } else {
+        win.emplace_back(cmd->beg, cmd->end);
+    }
+    // ---- the 64-position blocks of the batch the windows touch
+    const int64_t pos0 = hp->pos0, pend = (int64_t)hp->pos0 + hp->n_sites;
+    int64_t lo = pend, hi = pos0;
+    for (auto &x : win) {
+        int64_t a = std::max<int64_t>(x.first, pos0), b = std::min<int64_t>(x.second, pend);
+        if (a < b) {
+            lo = std::min(lo, a);
+            hi = std::max(hi, b);
+        }
+    }
+    std::vector<uint64_t> boff;
+    const uint64_t *hboff = hp->block_off;
+    const uint32_t nblk_all = (hp->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
+    if (!hboff) {
+        boff.assign(nblk_all + 1, 0);
+        uint64_t run = 0;
+        for (uint32_t b = 0; b < nblk_all; ++b) {
+            boff[b] = run;
+            const uint32_t s1 = std::min<uint32_t>(hp->n_sites, (b + 1) * pbg::kSiteBlock);
+            for (size_t i = (size_t)b * pbg::kSiteBlock * n; i < (size_t)s1 * n; ++i) run += hp->depth[i];
+        }
+        boff[nblk_all] = run;
+        hboff = boff.data();
+    }
+    uint32_t blo = 0, bhi = 0;
+    if (lo < hi) {
+        blo = (uint32_t)((lo - pos0) / pbg::kSiteBlock);
+        bhi = (uint32_t)((hi - pos0 + pbg::kSiteBlock - 1) / pbg::kSiteBlock);
+    }
+    const uint32_t dsites = lo < hi ? std::min<uint32_t>(hp->n_sites, bhi * pbg::kSiteBlock) - blo * pbg::kSiteBlock : 0;
+    const int64_t dpos0 = pos0 + (int64_t)blo * pbg::kSiteBlock;
+    const uint64_t r0 = lo < hi ? hboff[blo] : 0, r1 = lo < hi ? hboff[bhi] : 0;
+    const uint32_t dblk = bhi - blo;
+
+    DevBuf d_ref, d_dep, d_boff, d_reads, d_rows, d_cb, d_win;
+    hipStream_t s = nullptr;
+    const int rb = c->row_bytes;
+    const bool is_snp = cmd->cmd == PBG_CMD_SNP;
+    if (dsites) {
+        std::vector<uint64_t> lb(dblk + 1);
+        for (uint32_t b = 0; b <= dblk; ++b) lb[b] = hboff[blo + b] - r0;
+        HIPCHK(c, d_ref.alloc(dsites));
+        HIPCHK(c, d_dep.alloc((size_t)dsites * n * 2));
+        HIPCHK(c, d_boff.alloc((dblk + 1) * 8));
+        HIPCHK(c, d_reads.alloc((r1 - r0) * 4));
+        HIPCHK(c, d_rows.alloc((size_t)dsites * rb));
+        HIPCHK(c, hipMemcpy(d_ref.p, hp->ref + (size_t)blo * pbg::kSiteBlock, dsites, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(d_dep.p, hp->depth + (size_t)blo * pbg::kSiteBlock * n, (size_t)dsites * n * 2,
+                            hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(d_boff.p, lb.data(), (dblk + 1) * 8, hipMemcpyHostToDevice));
+        if (r1 > r0) HIPCHK(c, hipMemcpy(d_reads.p, hp->reads + r0, (r1 - r0) * 4, hipMemcpyHostToDevice));
+        if (is_snp) HIPCHK(c, d_cb.alloc((size_t)dsites * n * 8));
+        pbg_pileup dp{dsites, (int32_t)dpos0, (const uint8_t *)d_ref.p, (const uint16_t *)d_dep.p,
+                      (const uint64_t *)d_boff.p, (const uint32_t *)d_reads.p};
+        int rc = pbg_call_sites(c, &dp, d_rows.p, is_snp ? (uint64_t *)d_cb.p : nullptr, s);
+        if (rc) return rc;
+        int herr = 0;
+        HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+        if (herr) return fail(c, PBG_E_ARG, "pileup block_off disagrees with depth[]");
+    }
+    std::string text;
+    if (is_snp) {
+        // print_popbam_snp (pop_snp.cpp:224-241) per window: segregating positions in order
+        std::vector<unsigned char> rows((size_t)dsites * rb);
+        std::vector<uint64_t> cb((size_t)dsites * n);
+        if (dsites) {
+            HIPCHK(c, hipMemcpy(rows.data(), d_rows.p, rows.size(), hipMemcpyDeviceToHost));
+            HIPCHK(c, hipMemcpy(cb.data(), d_cb.p, cb.size() * 8, hipMemcpyDeviceToHost));
+        }
+        for (auto &x : win)
+            for (int64_t p = std::max<int64_t>(x.first, dpos0); p < std::min<int64_t>(x.second, dpos0 + dsites); ++p) {
+                const size_t i = (size_t)(p - dpos0);
+                const unsigned char *r = rows.data() + i * rb;
+                const bool seg = (r[rb - 1] >> 7) & 1;
+                if (seg) pbg::format_snp_site(text, *cmd, n, (int32_t)p, hp->ref[p - pos0] & 0x7f, cb.data() + i * n);
+            }
+    } else {
+        uint32_t stats = 0;
+        switch (cmd->cmd) {
+            case PBG_CMD_NUCDIV: stats = PBG_S_NUCDIV; break;
+            case PBG_CMD_SFS: stats = PBG_S_SFS; break;
+            case PBG_CMD_LD: stats = cmd->output == 1 ? PBG_S_OMEGA : cmd->output == 2 ? PBG_S_WALL : PBG_S_ZNS; break;
+            case PBG_CMD_DIVERGE: stats = cmd->output == 1 ? PBG_S_DIV_POP : PBG_S_DIV_IND; break;
+            case PBG_CMD_HAPLO:
+                stats = cmd->output == 1 ? PBG_S_HAP_EHHS : cmd->output == 2 ? PBG_S_HAP_DXY : PBG_S_HAP_K;
+                break;
+            default: return fail(c, PBG_E_ARG, "unsupported subcommand");
+        }
+        const uint32_t nw = (uint32_t)win.size();
+        // row ranges: clip each window to the uploaded rows (positions outside have no callback)
+        std::vector<pbg_window> rw(nw);
+        for (uint32_t i = 0; i < nw; ++i) {
+            int64_t a = std::min<int64_t>(std::max<int64_t>(win[i].first, dpos0), dpos0 + dsites);
+            int64_t b = std::min<int64_t>(std::max<int64_t>(win[i].second, a), dpos0 + dsites);
+            rw[i].beg = (int32_t)(a - dpos0);
+            rw[i].end = (int32_t)(b - dpos0);
+        }
+        const int npairs = std::max(1, np * (np - 1));
+        const size_t szw = nw, szp = (size_t)nw * np, szq = (size_t)nw * npairs, szn = (size_t)nw * n;
+        DevBuf o_ns, o_seg, o_d1, o_d2, o_d3, o_i1, o_i2, o_i3;
+        HIPCHK(c, d_win.alloc(nw * sizeof(pbg_window)));
+        HIPCHK(c, hipMemcpy(d_win.p, rw.data(), nw * sizeof(pbg_window), hipMemcpyHostToDevice));
+        HIPCHK(c, o_ns.alloc(szw * 4));
+        HIPCHK(c, o_seg.alloc(szw * 4));
+        HIPCHK(c, o_d1.alloc(std::max(szq, std::max(szp, szn)) * 8));
+        HIPCHK(c, o_d2.alloc(std::max(szq, szp) * 8));
+        HIPCHK(c, o_d3.alloc(szp * 8));
+        HIPCHK(c, o_i1.alloc(szp * 4));
+        HIPCHK(c, o_i2.alloc(szp * 4));
+        HIPCHK(c, o_i3.alloc(szq * 4));
+        pbg_window_out O{};
+        O.num_sites = (int32_t *)o_ns.p;
+        O.segsites = (int32_t *)o_seg.p;
+        double *d1 = (double *)o_d1.p, *d2 = (double *)o_d2.p, *d3 = (double *)o_d3.p;
+        int32_t *i1 = (int32_t *)o_i1.p, *i2 = (int32_t *)o_i2.p, *i3 = (int32_t *)o_i3.p;
+        switch (stats) {
+            case PBG_S_NUCDIV: O.pi = d1; O.dxy = d2; break;
+            case PBG_S_SFS: O.td = d1; O.fwh = d2; break;
+            case PBG_S_ZNS: case PBG_S_OMEGA: O.ld_snps = i1; O.ld_val = d1; break;
+            case PBG_S_WALL: O.ld_snps = i1; O.ld_val = d1; O.ld_q = d2; break;
+            case PBG_S_DIV_IND: O.div_ind = d1; break;
+            case PBG_S_DIV_POP: O.div_fixed = i1; O.div_seg = i2; O.div_pop = d1; break;
+            case PBG_S_HAP_K: O.nhaps = i1; O.hap_val = d1; break;
+            case PBG_S_HAP_EHHS: O.hap_val = d1; break;
+            case PBG_S_HAP_DXY: O.hap_val = d3; O.hap_dxy = d1; O.hap_min = i3; break;
+        }
+        pbg_stat_opts so{stats, cmd->min_freq, cmd->outidx, cmd->jc};
+        // an all-empty batch still needs one addressable row for the kernel's pointer
+        DevBuf dummy;
+        const void *rows_p = d_rows.p;
+        if (!rows_p) {
+            HIPCHK(c, dummy.alloc(16));
+            HIPCHK(c, hipMemset(dummy.p, 0, 16));
+            rows_p = dummy.p;
+        }
+        int rc = pbg_window_stats(c, rows_p, dsites, (const pbg_window *)d_win.p, nw, &so, &O, s);
+        if (rc) return rc;
+        HIPCHK(c, hipDeviceSynchronize());
+        std::vector<int32_t> h_ns(szw), h_seg(szw), h_i1(szp), h_i2(szp), h_i3(szq);
+        std::vector<double> h_d1(std::max(szq, std::max(szp, szn))), h_d2(std::max(szq, szp)), h_d3(szp);
+        HIPCHK(c, hipMemcpy(h_ns.data(), o_ns.p, szw * 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(h_seg.data(), o_seg.p, szw * 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(h_i1.data(), o_i1.p, szp * 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(h_i2.data(), o_i2.p, szp * 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(h_i3.data(), o_i3.p, szq * 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(h_d1.data(), o_d1.p, h_d1.size() * 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(h_d2.data(), o_d2.p, h_d2.size() * 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(h_d3.data(), o_d3.p, h_d3.size() * 8, hipMemcpyDeviceToHost));
+        pbg::WindowHost wh;
+        for (uint32_t i = 0; i < nw; ++i) {
+            wh.beg = win[i].first;
+            wh.end = win[i].second;
+            wh.num_sites = h_ns[i];
+            wh.segsites = h_seg[i];
+            auto slice = [](const auto &v, size_t off, size_t cnt) {
+                using T = typename std::decay_t<decltype(v)>::value_type;
+                return std::vector<T>(v.begin() + off, v.begin() + off + cnt);
+            };
+            switch (stats) {
+                case PBG_S_NUCDIV: wh.pi = slice(h_d1, i * np, np); wh.dxy = slice(h_d2, i * npairs, npairs); break;
+                case PBG_S_SFS: wh.td = slice(h_d1, i * np, np); wh.fwh = slice(h_d2, i * np, np); break;
+                case PBG_S_ZNS: case PBG_S_OMEGA:
+                    wh.ld_snps = slice(h_i1, i * np, np); wh.ld_val = slice(h_d1, i * np, np); break;
+                case PBG_S_WALL:
+                    wh.ld_snps = slice(h_i1, i * np, np); wh.ld_val = slice(h_d1, i * np, np);
+                    wh.ld_q = slice(h_d2, i * np, np); break;
+                case PBG_S_DIV_IND: wh.div_ind = slice(h_d1, i * n, n); break;
+                case PBG_S_DIV_POP:
+                    wh.div_fixed = slice(h_i1, i * np, np); wh.div_seg = slice(h_i2, i * np, np);
+                    wh.div_pop = slice(h_d1, i * np, np); break;
+                case PBG_S_HAP_K: wh.nhaps = slice(h_i1, i * np, np); wh.hap_val = slice(h_d1, i * np, np); break;
+                case PBG_S_HAP_EHHS: wh.hap_val = slice(h_d1, i * np, np); break;
+                case PBG_S_HAP_DXY:
+                    wh.hap_val = slice(h_d3, i * np, np); wh.hap_dxy = slice(h_d1, i * npairs, npairs);
+                    wh.hap_min = slice(h_i3, i * npairs, npairs); break;
+            }
+            pbg::format_window(text, *cmd, n, np, c->dp.flag, wh);
+        }
+    }
+    if (needed) *needed = text.size() + 1;
+    if (text.size() + 1 > cap) return fail(c, PBG_E_RANGE, "output buffer too small");
+    std::memcpy(out, text.c_str(), text.size() + 1);
+    return (long)text.size();
+}
+
+long pbg_format(const pbg_ctx *c, const pbg_cmd *cmd, const pbg_window_out *ho, uint32_t n_win, const int32_t *wbeg,
+                const int32_t *wend, char *out, size_t cap, size_t *needed) {
+    if (!c || !cmd || !ho || !wbeg || !wend || (!out && cap)) return fail(const_cast<pbg_ctx *>(c), PBG_E_ARG, "null argument");
+    const int n = c->dp.n, np = c->dp.npops, npairs = std::max(1, np * (np - 1));
+    std::string text;
+    pbg::WindowHost wh;
+    auto take = [](auto *src, size_t off, size_t cnt) {
+        using T = std::remove_cv_t<std::remove_pointer_t<decltype(src)>>;
+        return src ? std::vector<T>(src + off, src + off + cnt) : std::vector<T>(cnt, T());
+    };
+    for (uint32_t i = 0; i < n_win; ++i) {
+        wh.beg = wbeg[i];
+        wh.end = wend[i];
+        wh.num_sites = ho->num_sites ? ho->num_sites[i] : 0;
+        wh.segsites = ho->segsites ? ho->segsites[i] : 0;
+        wh.pi = take(ho->pi, (size_t)i * np, np);
+        wh.dxy = take(ho->dxy, (size_t)i * npairs, npairs);
+        wh.td = take(ho->td, (size_t)i * np, np);
+        wh.fwh = take(ho->fwh, (size_t)i * np, np);
+        wh.ld_snps = take(ho->ld_snps, (size_t)i * np, np);
+        wh.ld_val = take(ho->ld_val, (size_t)i * np, np);
+        wh.ld_q = take(ho->ld_q, (size_t)i * np, np);
+        wh.div_ind = take(ho->div_ind, (size_t)i * n, n);
+        wh.div_fixed = take(ho->div_fixed, (size_t)i * np, np);
+        wh.div_seg = take(ho->div_seg, (size_t)i * np, np);
+        wh.div_pop = take(ho->div_pop, (size_t)i * np, np);
+        wh.nhaps = take(ho->nhaps, (size_t)i * np, np);
+        wh.hap_val = take(ho->hap_val, (size_t)i * np, np);
+        wh.hap_dxy = take(ho->hap_dxy, (size_t)i * npairs, npairs);
+        wh.hap_min = take(ho->hap_min, (size_t)i * npairs, npairs);
+        pbg::format_window(text, *cmd, n, np, c->dp.flag, wh);
+    }
+    if (needed) *needed = text.size() + 1;
+    if (text.size() + 1 > cap) return fail(const_cast<pbg_ctx *>(c), PBG_E_RANGE, "output buffer too small");
+    std::memcpy(out, text.c_str(), text.size() + 1);
+    return (long)text.size();
+}
+
+}  // extern "C"

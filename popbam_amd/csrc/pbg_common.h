@@ -1,0 +1,112 @@
+// pbg_common.h -- types shared by the host orchestration and the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/popbam_gpu.h"
+
+namespace pbg {
+
+constexpr int kBlockThreads = 256;     // 4 wave64 per workgroup
+constexpr int kSiteBlock = PBG_SITE_BLOCK;
+constexpr int kFastKeys = 16;          // register sort-network width in the call kernel
+
+// Parameters passed by value to the kernels (kernarg segment).
+struct DevParams {
+    int32_t n, npops;
+    uint64_t pop_mask[PBG_MAX_POPS];
+    int32_t pop_n[PBG_MAX_POPS];
+    int32_t min_depth, max_depth, min_rmsQ, min_snpQ, min_mapQ, min_baseQ;
+    uint32_t flag;
+};
+
+// Host-built tables resident in HBM for the lifetime of a context.
+struct DevTables {
+    const double *fk;     // [256]            fk[n]   (pop_utils.cpp:216-219)
+    const double *beta;   // [64*256*256]     beta[q<<16|n<<8|k] (pop_utils.cpp:230-245)
+    const double *lhet;   // [256*256]        lhet[n<<8|k] (pop_utils.cpp:248-251)
+    const double *a1, *a2, *e1, *e2;          // Tajima/Fay-Wu constants (pop_sfs.cpp:511-571)
+    const double *r2;     // concatenated per-population r^2 tables, see r2_off
+    int32_t r2_off[PBG_MAX_POPS];             // offset of population p's (n_p+1)^3 table
+};
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// Synthetic pileup (benchmark workload): site hash keyed on (seed, pos).
+struct SynthSite {
+    uint64_t h;
+    int ref_idx, alt, snp;
+    uint32_t f16;
+};
+__host__ __device__ inline SynthSite synth_site(uint64_t seed, uint64_t pos) {
+    SynthSite s;
+    s.h = splitmix64(seed ^ splitmix64(pos));
+    s.ref_idx = (int)(s.h & 3);
+    s.snp = ((s.h >> 2) & 0x3FF) < 12;          // theta ~ 0.012
+    s.alt = (s.ref_idx + 1 + (int)((s.h >> 12) % 3)) & 3;
+    s.f16 = (uint32_t)((s.h >> 16) & 0xFFFF);   // derived allele frequency
+    return s;
+}
+__host__ __device__ inline uint64_t synth_sample_hash(const SynthSite &s, int sample) {
+    return splitmix64(s.h ^ (0xD1B54A32D192ED03ULL * (uint64_t)(sample + 1)));
+}
+__host__ __device__ inline int synth_depth(uint64_t hs, int mean_depth) {
+    // binomial(2D, 1/2): popcount of 2D random bits (mean D), D <= 32
+    uint64_t bits = splitmix64(hs ^ 0x5851F42D4C957F2DULL);
+    int nb = 2 * mean_depth;
+    uint64_t m = nb >= 64 ? ~0ULL : ((1ULL << nb) - 1);
+    return __builtin_popcountll(bits & m);
+}
+__host__ __device__ inline uint32_t synth_read(const SynthSite &s, uint64_t hs, int r) {
+    int a0 = (s.snp && (uint32_t)(hs & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
+    int a1 = (s.snp && (uint32_t)((hs >> 16) & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
+    uint64_t hr = splitmix64(hs + (uint64_t)r + 1);
+    int base = (hr & 1) ? a1 : a0;
+    if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((hr >> 8) % 3)) & 3;   // ~0.8% errors
+    uint32_t bq = 20 + (uint32_t)((hr >> 16) % 21);                               // 20..40
+    uint32_t strand = (uint32_t)((hr >> 40) & 1);
+    return bq | (60u << 8) | ((1u << base) << 16) | (strand << 20);
+}
+__host__ __device__ inline uint8_t synth_ref_char(const SynthSite &s) { return (uint8_t)"ACGT"[s.ref_idx]; }
+
+constexpr int kSegCap = 2048;        // segregating rows kept in LDS per window
+constexpr int kPlaneCap = 1024;      // bitplane words kept in LDS (n * words)
+
+// Per-window global workspace slice (u64 units), used only when a window outgrows LDS or
+// for the omega / Wall lists: [seg rows: len+1][bitplanes: n*(len/64+2)][lists: np*(len+1)]
+__host__ __device__ inline uint64_t ws_plane_off(int64_t len) { return (uint64_t)len + 1; }
+__host__ __device__ inline uint64_t ws_list_off(int64_t len, int n) {
+    return ws_plane_off(len) + (uint64_t)n * (uint64_t)(len / 64 + 2);
+}
+__host__ __device__ inline uint64_t ws_slice(int64_t len, int n, int np) {
+    return ws_list_off(len, n) + (uint64_t)np * (uint64_t)(len + 1);
+}
+
+struct StatsArgs {
+    uint32_t stats;
+    int32_t min_freq, outidx, jc;
+    const pbg_window *wins;
+    const uint64_t *ws_off;          // per-window offset into ws (u64 units), for big windows
+    uint64_t *ws;                    // global workspace
+    pbg_window_out out;
+};
+
+// kernel launchers (defined in call_kernel.hip / stats_kernel.hip)
+hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, uint32_t n_sites,
+                             const uint8_t *ref, const uint16_t *depth, const uint64_t *block_off,
+                             const uint32_t *reads, uint32_t cap, void *rows, uint64_t *cb, int *err,
+                             hipStream_t stream);
+size_t call_sites_lds_bytes(int n, uint32_t cap);
+hipError_t launch_synth_depth(uint64_t seed, int mean_depth, int n, uint32_t n_sites, uint8_t *ref,
+                              uint16_t *depth, uint64_t *block_tot, hipStream_t stream);
+hipError_t launch_synth_reads(uint64_t seed, int mean_depth, int n, uint32_t n_sites, const uint16_t *depth,
+                              const uint64_t *block_off, uint32_t *reads, hipStream_t stream);
+hipError_t launch_window_stats(int row_bytes, const DevParams &P, const DevTables &T, const void *rows,
+                               uint32_t n_rows, uint32_t n_win, const StatsArgs &A, hipStream_t stream);
+
+}  // namespace pbg

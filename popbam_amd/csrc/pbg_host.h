@@ -1,0 +1,33 @@
+// pbg_host.h -- host-side internals of libpopbam_gpu.so (not part of the C-ABI).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/popbam_gpu.h"
+
+namespace pbg {
+
+void build_errmod_tables(std::vector<double> &fk, std::vector<double> &beta, std::vector<double> &lhet);
+void build_sfs_constants(int n, std::vector<double> &a1, std::vector<double> &a2, std::vector<double> &e1,
+                         std::vector<double> &e2);
+void build_r2_table(int n_pop, std::vector<double> &t);
+
+// Host copies of one window's results, as print_<stat> needs them.
+struct WindowHost {
+    int32_t beg = 0, end = 0;       // contig coordinates [beg, end)
+    int32_t num_sites = 0, segsites = 0;
+    std::vector<double> pi, dxy, td, fwh, ld_val, ld_q, div_ind, div_pop, hap_val, hap_dxy;
+    std::vector<int32_t> ld_snps, div_fixed, div_seg, nhaps, hap_min;
+};
+
+// print_nucdiv / print_sfs / print_ld / print_diverge / print_haplo (TSV, byte-identical)
+void format_window(std::string &out, const pbg_cmd &cmd, int n_samples, int n_pops, uint32_t flag,
+                   const WindowHost &w);
+
+// print_popbam_snp (pop_snp.cpp:224-241) for one position's consensus words
+void format_snp_site(std::string &out, const pbg_cmd &cmd, int n_samples, int32_t pos, unsigned char refc,
+                     const uint64_t *cb);
+
+}  // namespace pbg

@@ -1,0 +1,479 @@
+// stats_kernel.hip -- per-window population-genetics statistics on gfx950.
+//
+// One workgroup (256 threads) per window.  Rows of the window are streamed once from HBM
+// (coalesced, row_bytes per position); counted positions are tallied with wave ballots and
+// the segregating rows are compacted, in order, into LDS (global workspace when a window has
+// more than kSegCap of them).  Derived-allele bitplanes per sample are built with wave64
+// ballots (one u64 word = 64 segregating sites), which turns the pairwise-difference matrix
+// (calc_diff_matrix, pop_nucdiv.cpp:242-256) into popcounts of XORed words.
+//
+// The floating-point epilogues run in single lanes in exactly the reference's order
+// (sequential double sums; x86 rounding reproduced: -ffp-contract=off, IEEE div/sqrt), so
+// integer outputs and all ZnS / omega / D / H / pi values are bit-identical:
+//   nucdiv   calc_nucdiv           pop_nucdiv.cpp:206-239 (+ /num_sites of print_nucdiv)
+//   sfs      calc_sfs              pop_sfs.cpp:227-291
+//   ld       calc_zns / calc_omegamax / calc_wall   pop_ld.cpp:201-458
+//   diverge  calc_diverge + print  pop_diverge.cpp:220-257, 496-574
+//   haplo    calc_nhaps / calc_ehhs / calc_minDxy    pop_haplo.cpp:208-363
+#include "pbg_common.h"
+
+namespace pbg {
+
+namespace {
+
+template <int RB>
+__device__ __forceinline__ void load_row(const void *rows, int64_t i, uint64_t &types, bool &counted, bool &seg, int n) {
+    if constexpr (RB == 16) {
+        ulonglong2 v = reinterpret_cast<const ulonglong2 *>(rows)[i];
+        types = v.x;
+        counted = (v.y >> 62) & 1;
+        seg = (v.y >> 63) & 1;
+    } else {
+        uint64_t v;
+        if constexpr (RB == 2) v = reinterpret_cast<const uint16_t *>(rows)[i];
+        else if constexpr (RB == 4) v = reinterpret_cast<const uint32_t *>(rows)[i];
+        else v = reinterpret_cast<const uint64_t *>(rows)[i];
+        constexpr int W = RB * 8;
+        counted = (v >> (W - 2)) & 1;
+        seg = (v >> (W - 1)) & 1;
+        types = v & ((W == 64) ? 0x3FFFFFFFFFFFFFFFULL : ((1ULL << (W - 2)) - 1));
+    }
+}
+
+__device__ __forceinline__ unsigned pc(uint64_t x) { return (unsigned)__popcll(x); }
+
+// x86 SSE produces the "default NaN" (sign bit set) for invalid operations; glibc prints it
+// as "-nan".  Canonicalise device NaNs the same way before they reach the formatter.
+__device__ __forceinline__ double x86nan(double v) { return (v != v) ? __longlong_as_double(0xFFF8000000000000LL) : v; }
+
+// r^2 of pop_ld.cpp:239-243 from the host table (same expression, same rounding)
+__device__ __forceinline__ double r2lookup(const DevTables &T, int p, int np1, unsigned m1, unsigned m2, unsigned c11) {
+    return T.r2[T.r2_off[p] + ((int)m1 * np1 + (int)m2) * np1 + (int)c11];
+}
+
+}  // namespace
+
+template <int RB>
+__global__ __launch_bounds__(kBlockThreads) void window_stats_kernel(DevParams P, DevTables T, const void *__restrict__ rows,
+                                                                     uint32_t n_rows, uint32_t n_win, StatsArgs A) {
+    __shared__ uint64_t s_seg[kSegCap];
+    __shared__ uint64_t s_plane[kPlaneCap];
+    __shared__ uint16_t s_diff[PBG_MAX_SAMPLES * PBG_MAX_SAMPLES];
+    __shared__ uint32_t s_wcnt[kBlockThreads / 64][2];
+    __shared__ int32_t s_scratch[PBG_MAX_POPS * (PBG_MAX_SAMPLES + 2)];
+    __shared__ int32_t s_ns, s_S;
+
+    const uint32_t w = blockIdx.x;
+    if (w >= n_win) return;
+    const int n = P.n, np = P.npops;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t wb = A.wins[w].beg, we = A.wins[w].end;
+    const int64_t len = we > wb ? we - wb : 0;
+
+    // ---- pass 1: counted / segregating totals
+    uint32_t my_c = 0, my_s = 0;
+    for (int64_t i = tid; i < len; i += kBlockThreads) {
+        uint64_t t;
+        bool c, s;
+        load_row<RB>(rows, wb + i, t, c, s, n);
+        my_c += c;
+        my_s += s;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        my_c += __shfl_down(my_c, o, 64);
+        my_s += __shfl_down(my_s, o, 64);
+    }
+    if (lane == 0) { s_wcnt[wv][0] = my_c; s_wcnt[wv][1] = my_s; }
+    __syncthreads();
+    if (tid == 0) {
+        int a = 0, b = 0;
+        for (int k = 0; k < kBlockThreads / 64; ++k) { a += (int)s_wcnt[k][0]; b += (int)s_wcnt[k][1]; }
+        s_ns = a;
+        s_S = b;
+    }
+    __syncthreads();
+    const int num_sites = s_ns, S = s_S;
+    uint64_t *seg = (S <= kSegCap) ? s_seg : (A.ws + A.ws_off[w]);
+
+    // ---- pass 2: ordered compaction of segregating rows (ballot + cross-wave prefix)
+    {
+        int base = 0;
+        for (int64_t c0 = 0; c0 < len; c0 += kBlockThreads) {
+            int64_t i = c0 + tid;
+            uint64_t t = 0;
+            bool c = false, s = false;
+            if (i < len) load_row<RB>(rows, wb + i, t, c, s, n);
+            uint64_t m = __ballot(s);
+            int before = (int)__popcll(m & ((1ULL << lane) - 1));
+            __syncthreads();
+            if (lane == 0) s_wcnt[wv][0] = (uint32_t)__popcll(m);
+            __syncthreads();
+            int wofs = 0, tot = 0;
+            for (int k = 0; k < kBlockThreads / 64; ++k) {
+                if (k < wv) wofs += (int)s_wcnt[k][0];
+                tot += (int)s_wcnt[k][0];
+            }
+            if (s) seg[base + wofs + before] = t;
+            base += tot;
+        }
+    }
+    __syncthreads();
+
+    // types of the j-th segregating site: seg[j] (== types[hap.idx[j]] in the reference)
+    const int nwords = S > 0 ? (S + 63) / 64 : 1;
+    const bool need_planes = (A.stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY)) != 0;
+    uint64_t *plane = nullptr;
+    if (need_planes) {
+        plane = (n * nwords <= kPlaneCap) ? s_plane : (A.ws + A.ws_off[w] + ws_plane_off(len));
+        // plane[v*nwords + k] bit b = sample v derived at segregating site 64k+b (hap.seq)
+        for (int k = wv; k < nwords; k += kBlockThreads / 64) {
+            int j = k * 64 + lane;
+            uint64_t t = j < S ? seg[j] : 0;
+            for (int v = 0; v < n; ++v) {
+                uint64_t m = __ballot((t >> v) & 1);
+                if (lane == 0) plane[v * nwords + k] = m;
+            }
+        }
+        __syncthreads();
+        // calc_diff_matrix: u16 accumulation (wraps, Appendix A.7)
+        const int npair = n * n;
+        for (int pr = tid; pr < npair; pr += kBlockThreads) {
+            int v = pr / n, u = pr - v * n;
+            uint32_t d = 0;
+            if (v != u)
+                for (int k = 0; k < nwords; ++k) d += pc(plane[v * nwords + k] ^ plane[u * nwords + k]);
+            s_diff[pr] = (uint16_t)(d & 0xFFFF);
+        }
+        __syncthreads();
+    }
+
+    const pbg_window_out &O = A.out;
+    if (tid == 0) {
+        if (O.num_sites) O.num_sites[w] = num_sites;
+        if (O.segsites) O.segsites[w] = S;
+    }
+    const int npairs = np * (np - 1);
+
+    // ---- nucdiv (one lane): integer sums are exact in double, as in the reference
+    if ((A.stats & PBG_S_NUCDIV) && tid == 0) {
+        for (int i = 0; i < np; i++)
+            for (int j = i; j < np; j++) {
+                double acc = 0.0;
+                for (int v = 0; v < n - 1; v++)
+                    for (int u = v + 1; u < n; u++)
+                        if (((P.pop_mask[i] >> v) & 1) && ((P.pop_mask[j] >> u) & 1)) acc += (double)s_diff[v * n + u];
+                if (i != j) {
+                    acc *= 1.0 / (double)(P.pop_n[i] * P.pop_n[j]);
+                    if (O.dxy) O.dxy[(size_t)w * npairs + i * np + (j - (i + 1))] = x86nan(acc / num_sites);
+                } else {
+                    acc *= 2.0 / (double)(P.pop_n[i] * (P.pop_n[i] - 1));
+                    if (acc != acc) acc = 0.0;
+                    if (O.pi) O.pi[(size_t)w * np + i] = x86nan(acc / num_sites);
+                }
+            }
+    }
+
+    // ---- sfs (lane per population)
+    if ((A.stats & PBG_S_SFS) && tid >= 64 && tid < 64 + np) {
+        const int i = tid - 64;
+        const int nn = P.pop_n[i];
+        int *sfs = s_scratch + i * (PBG_MAX_SAMPLES + 2);
+        for (int j = 0; j <= nn; ++j) sfs[j] = 0;
+        int S_i = 0;
+        for (int j = 0; j < S; j++) {
+            uint64_t t = seg[j];
+            uint64_t pt = t & P.pop_mask[i];
+            unsigned freq;
+            if ((P.flag & PBG_F_OUTGROUP) && ((t >> A.outidx) & 1)) freq = (unsigned)(uint16_t)(nn - (int)pc(pt));
+            else freq = pc(pt);
+            ++sfs[freq];
+            if (freq > 0 && (int)freq < nn) ++S_i;
+        }
+        double td = 0.0, fwh = 0.0;
+        if (S_i > 0 && nn > 1) {
+            const double a1 = T.a1[nn], a2 = T.a2[nn], e1 = T.e1[nn], e2 = T.e2[nn], a2n1 = T.a2[nn + 1];
+            for (int j = 1; j < nn; j++) {
+                td += sfs[j] * (((2.0 * j * (nn - j)) / (nn * (nn - 1))) - (1.0 / a1));
+                fwh += sfs[j] * ((1.0 / a1) - ((double)j / (nn - 1)));
+            }
+            td /= sqrt(e1 * S_i + e2 * S_i * (S_i - 1));
+            fwh /= sqrt(((nn - 2) * (S_i / a1) / (6.0 * (nn - 1))) +
+                                  ((S_i * (S_i - 1) / ((a1 * a1) + a2)) *
+                                   (18.0 * (nn * nn) * (3.0 * nn + 2.0) * a2n1 - (88.0 * nn * nn * nn + 9.0 * (nn * nn) - 13.0 * nn + 6.0)) /
+                                   (9.0 * nn * ((nn - 1) * (nn - 1)))));
+        } else {
+            td = __longlong_as_double(0x7FF8000000000000LL);
+            fwh = td;
+        }
+        if (O.td) O.td[(size_t)w * np + i] = td;
+        if (O.fwh) O.fwh[(size_t)w * np + i] = fwh;
+    }
+
+    // ---- ld ZnS (lane per population), pop_ld.cpp:201-252
+    if ((A.stats & PBG_S_ZNS) && tid >= 128 && tid < 128 + np) {
+        const int i = tid - 128;
+        const int nn = P.pop_n[i], np1 = nn + 1, mf = A.min_freq;
+        const uint64_t pm = P.pop_mask[i];
+        int ns = 0;
+        double zns = 0.0;
+        if (S >= 1) {
+            for (int j = 0; j < S - 1; j++) {
+                uint64_t t1 = seg[j] & pm;
+                unsigned m1 = pc(t1);
+                if ((int)m1 >= mf && (int)m1 <= nn - mf) {
+                    ++ns;
+                    for (int k = j + 1; k < S; k++) {
+                        uint64_t t2 = seg[k] & pm;
+                        unsigned m2 = pc(t2);
+                        if ((int)m2 >= mf && (int)m2 <= nn - mf) zns += r2lookup(T, i, np1, m1, m2, pc(t1 & t2));
+                    }
+                }
+            }
+            ++ns;
+            zns *= 2.0 / (ns * (ns - 1));
+        }
+        if (O.ld_snps) O.ld_snps[(size_t)w * np + i] = ns;
+        if (O.ld_val) O.ld_val[(size_t)w * np + i] = x86nan(zns);
+    }
+
+    // ---- ld omega_max (lane per population), pop_ld.cpp:254-373: r^2 entries are looked
+    // up on the fly from the compressed variable-site list (no S x S matrix)
+    if ((A.stats & PBG_S_OMEGA) && tid >= 128 && tid < 128 + np) {
+        const int i = tid - 128;
+        const int nn = P.pop_n[i], np1 = nn + 1, mf = A.min_freq;
+        const uint64_t pm = P.pop_mask[i];
+        int ns = 0;
+        double om = 0.0;
+        if (S >= 1) {
+            // variable sites among the first S-1 (count1 indices); the last segregating
+            // site gets a count2 index if variable (V total)
+            int V = 0;
+            for (int j = 0; j < S; j++) {
+                unsigned m = pc(seg[j] & pm);
+                if ((int)m >= mf && (int)m <= nn - mf) {
+                    if (j < S - 1) ++ns;
+                    ++V;
+                }
+            }
+            ++ns;
+            // r2(a,b), a<b, variable-site indices; 0 when either index >= V
+            // variable types into the workspace (ws slice after planes) or LDS scratch
+            uint64_t *vt = A.ws + A.ws_off[w] + ws_list_off(len, n) + (uint64_t)i * (uint64_t)(len + 1);
+            {
+                int c = 0;
+                for (int j = 0; j < S; j++) {
+                    uint64_t t = seg[j] & pm;
+                    unsigned m = pc(t);
+                    if ((int)m >= mf && (int)m <= nn - mf) vt[c++] = t;
+                }
+            }
+            auto r2 = [&](int a, int b) -> double {
+                if (a >= V || b >= V) return 0.0;
+                uint64_t ta = vt[a], tb = vt[b];
+                return r2lookup(T, i, np1, pc(ta), pc(tb), pc(ta & tb));
+            };
+            double sl = 0, sr = 0, sb = 0;
+            for (int ii = 1; ii < ns - 1; ii++) {
+                for (int k = 0; k < ii; k++)
+                    for (int m = k + 1; m <= ii; m++) sl += r2(k, m);
+                for (int k = ii + 1; k < ns; k++)
+                    for (int m = 0; m <= ii; m++) sb += r2(m, k);
+                for (int k = ii + 1; k < ns - 1; k++)
+                    for (int m = k + 1; m < ns; m++) sr += r2(k, m);
+                int left = ii + 1, right = ns - left;
+                double omega = (sl + sr) / (((left * (left - 1)) / 2.0) + ((right * (right - 1)) / 2.0));
+                omega *= left * right / sb;
+                om = omega > om ? omega : om;
+            }
+        }
+        if (O.ld_snps) O.ld_snps[(size_t)w * np + i] = ns;
+        if (O.ld_val) O.ld_val[(size_t)w * np + i] = x86nan(om);
+    }
+
+    // ---- Wall's B / Q (one lane; last_type shared across populations, A.9)
+    if ((A.stats & PBG_S_WALL) && tid == 192) {
+        int ns[PBG_MAX_POPS], cong[PBG_MAX_POPS], part[PBG_MAX_POPS], nu[PBG_MAX_POPS];
+        for (int j = 0; j < np; j++) ns[j] = cong[j] = part[j] = nu[j] = 0;
+        uint64_t *uniq = A.ws + A.ws_off[w] + ws_list_off(len, n);   // np slices of (len+1)
+        uint64_t last_type = 0;
+        if (S >= 1) {
+            for (int i = 0; i < S; i++)
+                for (int j = 0; j < np; j++) {
+                    uint64_t t = seg[i];
+                    uint64_t type = t & P.pop_mask[j];
+                    uint64_t comp = ~t & P.pop_mask[j];
+                    uint64_t *u = uniq + (uint64_t)j * (uint64_t)(len + 1);
+                    if (type > 0 && type < P.pop_mask[j]) {
+                        if (ns[j] == 0) {
+                            u[nu[j]++] = type;
+                            last_type = type;
+                            ns[j]++;
+                        } else {
+                            if (type == last_type || comp == last_type) {
+                                cong[j]++;
+                                bool seen = false;
+                                for (int q = 0; q < nu[j]; q++) seen |= (u[q] == type) || (u[q] == comp);
+                                if (!seen) {
+                                    u[nu[j]++] = type;
+                                    part[j]++;
+                                }
+                            }
+                            ns[j]++;
+                            last_type = type;
+                        }
+                    }
+                }
+        }
+        for (int j = 0; j < np; j++) {
+            double b = 0.0, q = 0.0;
+            if (S >= 1) {
+                b = (double)cong[j] / (double)(ns[j] - 1);
+                q = (double)(cong[j] + part[j]) / ns[j];
+            }
+            if (O.ld_snps) O.ld_snps[(size_t)w * np + j] = ns[j];
+            if (O.ld_val) O.ld_val[(size_t)w * np + j] = x86nan(b);
+            if (O.ld_q) O.ld_q[(size_t)w * np + j] = x86nan(q);
+        }
+    }
+
+    // ---- diverge -o 0 (lane per sample): u16 accumulation of derived counts
+    if ((A.stats & PBG_S_DIV_IND) && tid < n) {
+        uint32_t d = 0;
+        for (int k = 0; k < nwords; ++k) d += pc(plane[tid * nwords + k]);
+        double pd = (double)(d & 0xFFFF) / num_sites;
+        double v = A.jc ? -0.75 * log(1.0 - pd * (4.0 / 3.0)) : pd;
+        if (O.div_ind) O.div_ind[(size_t)w * n + tid] = x86nan(v);
+    }
+    // ---- diverge -o 1 (lane per population)
+    if ((A.stats & PBG_S_DIV_POP) && tid >= 64 && tid < 64 + np) {
+        const int i = tid - 64, nn = P.pop_n[i];
+        int segs = 0;
+        uint32_t fixed = 0;
+        for (int j = 0; j < S; j++) {
+            uint64_t t = seg[j];
+            uint64_t pt = t & P.pop_mask[i];
+            unsigned freq;
+            if ((P.flag & PBG_F_OUTGROUP) && ((t >> A.outidx) & 1)) freq = (unsigned)(uint16_t)(nn - (int)pc(pt));
+            else freq = pc(pt);
+            if (freq > 0 && (int)freq < nn) ++segs;
+            else if ((int)freq == nn) ++fixed;
+        }
+        fixed &= 0xFFFF;
+        double pd = (P.flag & PBG_F_SUBSTITUTE) ? (double)fixed / num_sites : (double)(fixed + segs) / num_sites;
+        double v = A.jc ? -0.75 * log(1.0 - pd * (4.0 / 3.0)) : pd;
+        if (O.div_fixed) O.div_fixed[(size_t)w * np + i] = (int32_t)fixed;
+        if (O.div_seg) O.div_seg[(size_t)w * np + i] = segs;
+        if (O.div_pop) O.div_pop[(size_t)w * np + i] = x86nan(v);
+    }
+
+    // ---- haplo K / Kdiv and EHHS (lane per population)
+    if ((A.stats & (PBG_S_HAP_K | PBG_S_HAP_EHHS)) && tid >= 64 && tid < 64 + np) {
+        const int i = tid - 64, nelem = P.pop_n[i];
+        int nh = 0;
+        double hdiv;
+        int *b = s_scratch + i * (PBG_MAX_SAMPLES + 2);
+        if (nelem > 1) {
+            int c = 0;
+            for (int j = 0; j < n; j++)
+                if ((P.pop_mask[i] >> j) & 1) b[c++] = j;
+            // local indices j,k index the global diff matrix (A.11)
+            for (int j = 0; j < nelem - 1; j++)
+                for (int k = j + 1; k < nelem; k++)
+                    if (s_diff[j * n + k] == 0 && b[k] > b[j]) b[k] = j;
+            int ff = 0;
+            for (int j = 0; j < nelem; j++) {
+                int f = 0;
+                for (int q = 0; q < nelem; q++) f += b[q] == j;
+                if (f > 0) ++nh;
+                ff += f * f;
+            }
+            double sh = (double)(ff) / (double)(nelem * nelem);
+            hdiv = 1.0 - ((1.0 - sh) * (double)(nelem / (nelem - 1)));
+        } else {
+            nh = 1;
+            hdiv = 1.0;
+        }
+        if (A.stats & PBG_S_HAP_K) {
+            if (O.nhaps) O.nhaps[(size_t)w * np + i] = nh;
+            if (O.hap_val) O.hap_val[(size_t)w * np + i] = x86nan(1.0 - hdiv);
+        } else {
+            double e;
+            if (nelem < 4) {
+                e = __longlong_as_double(0x7FF8000000000000LL);
+            } else {
+                // max multiplicity among non-singleton partitions, ties -> smallest value
+                // (std::list sort + unique + remove, pop_haplo.cpp:273-313)
+                const uint64_t pm = P.pop_mask[i];
+                int best = 0;
+                uint64_t max_site = 0;
+                for (int j = 0; j < S; j++) {
+                    uint64_t pt = seg[j] & pm;
+                    unsigned f = pc(pt);
+                    if (!(f > 1 && (int)f < nelem - 1)) continue;
+                    int cnt = 0;
+                    for (int q = 0; q < S; q++) cnt += (seg[q] & pm) == pt;
+                    int part_count = cnt + 1;
+                    if (part_count > best || (part_count == best && pt < max_site)) {
+                        best = part_count;
+                        max_site = pt;
+                    }
+                }
+                unsigned popf = pc(max_site);
+                int pn = nelem;
+                double sh = (1.0 - ((double)((int)(popf * popf) + ((pn - (int)popf) * (pn - (int)popf))) / (pn * pn))) *
+                            (double)(pn / (pn - 1));
+                e = hdiv / (1.0 - sh);
+            }
+            if (O.hap_val) O.hap_val[(size_t)w * np + i] = e;
+        }
+    }
+
+    // ---- haplo -o 2: pi (not divided by num_sites), dxy and min pairwise differences
+    if ((A.stats & PBG_S_HAP_DXY) && tid == 0) {
+        for (int i = 0; i < np; i++)
+            for (int j = i; j < np; j++) {
+                double acc = 0.0;
+                int mn = 65535;   // UINT_MAX narrowed to u16 (A.7)
+                for (int v = 0; v < n - 1; v++)
+                    for (int u = v + 1; u < n; u++)
+                        if (((P.pop_mask[i] >> v) & 1) && ((P.pop_mask[j] >> u) & 1)) {
+                            acc += (double)s_diff[v * n + u];
+                            if (i != j) mn = mn < (int)s_diff[v * n + u] ? mn : (int)s_diff[v * n + u];
+                        }
+                if (i != j) {
+                    acc *= 1.0 / (double)(P.pop_n[i] * P.pop_n[j]);
+                    int pi = i * np + (j - (i + 1));
+                    if (O.hap_dxy) O.hap_dxy[(size_t)w * npairs + pi] = x86nan(acc);
+                    if (O.hap_min) O.hap_min[(size_t)w * npairs + pi] = mn;
+                } else {
+                    acc *= 2.0 / (double)(P.pop_n[i] * (P.pop_n[i] - 1));
+                    if (acc != acc) acc = 0.0;
+                    if (O.hap_val) O.hap_val[(size_t)w * np + i] = acc;
+                }
+            }
+    }
+}
+
+template __global__ void window_stats_kernel<2>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
+template __global__ void window_stats_kernel<4>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
+template __global__ void window_stats_kernel<8>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
+template __global__ void window_stats_kernel<16>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
+
+}  // namespace pbg
+
+namespace pbg {
+
+hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, const void *rows, uint32_t n_rows,
+                               uint32_t n_win, const StatsArgs &A, hipStream_t stream) {
+    if (n_win == 0) return hipSuccess;
+    dim3 g(n_win), b(kBlockThreads);
+    switch (rb) {
+        case 2: hipLaunchKernelGGL(window_stats_kernel<2>, g, b, 0, stream, P, T, rows, n_rows, n_win, A); break;
+        case 4: hipLaunchKernelGGL(window_stats_kernel<4>, g, b, 0, stream, P, T, rows, n_rows, n_win, A); break;
+        case 8: hipLaunchKernelGGL(window_stats_kernel<8>, g, b, 0, stream, P, T, rows, n_rows, n_win, A); break;
+        default: hipLaunchKernelGGL(window_stats_kernel<16>, g, b, 0, stream, P, T, rows, n_rows, n_win, A); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace pbg

@@ -1,0 +1,83 @@
+"""One `popbam <cmd>` invocation on the GPU (host-side mirror of main_<cmd>).
+
+`run_command` takes what the reference derives before its window loop -- parsed options
+(popbam_amd.options), the @RG sample model, the region -- plus the dense pileup batch the
+host side of the pileup callback produced, and returns the reference's stdout.  All
+compute runs in libpopbam_gpu.so (pbg_run); there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from . import options as opt
+
+
+def make_params(o: opt.Options, sm: opt.SampleModel) -> _lib.PbgParams:
+    masks, counts = sm.pop_masks()
+    if len(masks) > _lib.PBG_MAX_POPS:
+        raise opt.PopbamError("more than 16 populations")
+    p = _lib.PbgParams()
+    p.n_samples, p.n_pops = sm.n, len(masks)
+    for i, (m, c) in enumerate(zip(masks, counts)):
+        p.pop_mask[i], p.pop_n[i] = m, c
+    p.min_depth, p.max_depth = o.min_depth, o.max_depth
+    p.min_rmsQ, p.min_snpQ = o.min_rmsQ, o.min_snpQ
+    p.min_mapQ, p.min_baseQ = o.min_mapQ & 0xFF, o.min_baseQ & 0xFF
+    p.flag = o.flag
+    return p
+
+
+class _Cmd:
+    def __init__(self, o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, end: int):
+        c = _lib.PbgCmd()
+        c.cmd = opt.CMD_IDS[o.cmd]
+        c.output, c.min_sites, c.min_snps, c.min_freq = o.output, o.min_sites, o.min_snps, o.min_freq
+        c.outidx = 0
+        if o.flag & opt.BAM_OUTGROUP:
+            idx = [i for i, s in enumerate(sm.samples) if s == o.outgroup]
+            if not idx:
+                raise opt.PopbamError(f"Specified outgroup {o.outgroup} not found")
+            c.outidx = idx[-1]
+        c.jc = 1 if o.dist == "jc" else 0
+        c.windowed = 1 if o.flag & opt.BAM_WINDOW else 0
+        c.win_size = o.win_size
+        c.beg, c.end = beg, end
+        self._chr = chr_name.encode()
+        self._sn = (C.c_char_p * max(1, sm.n))(*[s.encode() for s in sm.samples])
+        self._pn = (C.c_char_p * max(1, len(sm.pops)))(*[p.encode() for p in sm.pops])
+        c.chr_name = self._chr
+        c.sample_names = C.cast(self._sn, C.POINTER(C.c_char_p))
+        c.pop_names = C.cast(self._pn, C.POINTER(C.c_char_p))
+        self.c = c
+
+
+def run_command(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, end: int, batch: dict,
+                pos0: int = 0, device: int = 0, ctx: _lib.Context | None = None) -> str:
+    """batch: {'ref': u8[n_sites], 'depth': u16[n_sites, n], 'reads': u32[...]} (host)."""
+    own = ctx is None
+    if own:
+        ctx = _lib.Context(make_params(o, sm), device)
+    try:
+        ref = np.ascontiguousarray(batch["ref"], dtype=np.uint8)
+        dep = np.ascontiguousarray(batch["depth"], dtype=np.uint16)
+        rd = np.ascontiguousarray(batch["reads"], dtype=np.uint32)
+        if rd.size == 0:
+            rd = np.zeros(1, np.uint32)
+        pl = _lib.PbgPileup(len(ref), pos0, ref.ctypes.data, dep.ctypes.data, None, rd.ctypes.data)
+        cmd = _Cmd(o, sm, chr_name, beg, end)
+        need = C.c_size_t(0)
+        cap = 1 << 20
+        while True:
+            buf = C.create_string_buffer(cap)
+            r = ctx.lib.pbg_run(ctx.h, C.byref(cmd.c), C.byref(pl), buf, cap, C.byref(need))
+            if r == _lib.PBG_E_RANGE and need.value > cap:
+                cap = need.value
+                continue
+            ctx.check(r, "pbg_run")
+            return buf.value.decode()
+    finally:
+        if own:
+            ctx.close()

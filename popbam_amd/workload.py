@@ -1,0 +1,152 @@
+"""HBM-resident synthetic workload + the device-side hot path (benchmark / scale tests).
+
+`SynthPileup` generates the counter-based synthetic pileup (splitmix64 keyed
+on (seed, position); depth ~ Binomial(2D, 1/2), baseQ 20..40, mapQ 60, ~0.8% errors,
+theta ~ 1.2% segregating) straight into device memory with the library's generator kernels.
+`HotPath` runs one step -- call kernel + window-statistics kernel -- on it.  torch is used
+only to own device memory and streams; all compute is in libpopbam_gpu.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+SITE_BLOCK = _lib.PBG_SITE_BLOCK
+
+
+def _ptr(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def stream_handle(stream: torch.cuda.Stream | None = None) -> int:
+    s = stream or torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def default_params(n_samples: int, n_pops: int = 2, **kw) -> _lib.PbgParams:
+    """Contiguous equal populations, reference default filters."""
+    p = _lib.PbgParams()
+    p.n_samples, p.n_pops = n_samples, n_pops
+    per = n_samples // n_pops
+    for i in range(n_samples):
+        pi = min(i // per, n_pops - 1)
+        p.pop_mask[pi] |= 1 << i
+        p.pop_n[pi] += 1
+    p.min_depth, p.max_depth, p.min_rmsQ, p.min_snpQ = 3, 255, 25, 25
+    p.min_mapQ, p.min_baseQ, p.flag = 13, 13, 0
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class SynthPileup:
+    def __init__(self, ctx: _lib.Context, n_sites: int, mean_depth: int = 10, seed: int = 0xC0FFEE02,
+                 device: str = "cuda"):
+        self.ctx, self.n_sites, self.mean_depth, self.seed = ctx, n_sites, mean_depth, seed
+        n = ctx.params.n_samples
+        nblk = (n_sites + SITE_BLOCK - 1) // SITE_BLOCK
+        self.ref = torch.empty(n_sites, dtype=torch.uint8, device=device)
+        self.depth = torch.empty(n_sites * n, dtype=torch.int16, device=device)
+        self.block_off = torch.zeros(nblk + 1, dtype=torch.int64, device=device)
+        nr = C.c_uint64(0)
+        s = stream_handle()
+        ctx.check(ctx.lib.pbg_synth_depth(ctx.h, seed, mean_depth, n_sites, _ptr(self.ref), _ptr(self.depth),
+                                          _ptr(self.block_off), C.byref(nr), s), "pbg_synth_depth")
+        self.n_reads = nr.value
+        self.reads = torch.empty(max(1, self.n_reads), dtype=torch.int32, device=device)
+        ctx.check(ctx.lib.pbg_synth_reads(ctx.h, seed, mean_depth, n_sites, _ptr(self.depth), _ptr(self.block_off),
+                                          _ptr(self.reads), s), "pbg_synth_reads")
+        torch.cuda.synchronize()
+
+    def pileup(self) -> _lib.PbgPileup:
+        return _lib.PbgPileup(self.n_sites, 0, _ptr(self.ref), _ptr(self.depth), _ptr(self.block_off),
+                              _ptr(self.reads))
+
+    def bytes_read_by_call(self) -> int:
+        """Algorithmic HBM bytes one call-kernel launch must move: every read record (4 B),
+        the depth matrix (2 B per site x sample), the reference byte, the block offsets, and
+        the packed rows it writes."""
+        n = self.ctx.params.n_samples
+        nblk = (self.n_sites + SITE_BLOCK - 1) // SITE_BLOCK
+        return 4 * self.n_reads + 2 * self.n_sites * n + self.n_sites + 8 * (nblk + 1) + \
+            self.ctx.row_bytes * self.n_sites
+
+
+def reference_windows(beg: int, end: int, win_size: int):
+    """main_<cmd> window list (pop_nucdiv.cpp:49, 63): [beg+cw*w, beg+(cw+1)*w-1)."""
+    nw = ((end - beg) - 1) // win_size
+    return [(beg + cw * win_size, (cw + 1) * win_size + beg - 1) for cw in range(nw)]
+
+
+class WindowOutputs:
+    """Device arrays for pbg_window_out (all statistics)."""
+
+    def __init__(self, n_win: int, n: int, np_: int, device: str = "cuda"):
+        npairs = max(1, np_ * (np_ - 1))
+        f64 = dict(dtype=torch.float64, device=device)
+        i32 = dict(dtype=torch.int32, device=device)
+        self.t = {
+            "num_sites": torch.zeros(n_win, **i32), "segsites": torch.zeros(n_win, **i32),
+            "pi": torch.zeros(n_win * np_, **f64), "dxy": torch.zeros(n_win * npairs, **f64),
+            "td": torch.zeros(n_win * np_, **f64), "fwh": torch.zeros(n_win * np_, **f64),
+            "ld_snps": torch.zeros(n_win * np_, **i32), "ld_val": torch.zeros(n_win * np_, **f64),
+            "ld_q": torch.zeros(n_win * np_, **f64), "div_ind": torch.zeros(n_win * n, **f64),
+            "div_fixed": torch.zeros(n_win * np_, **i32), "div_seg": torch.zeros(n_win * np_, **i32),
+            "div_pop": torch.zeros(n_win * np_, **f64), "nhaps": torch.zeros(n_win * np_, **i32),
+            "hap_val": torch.zeros(n_win * np_, **f64), "hap_dxy": torch.zeros(n_win * npairs, **f64),
+            "hap_min": torch.zeros(n_win * npairs, **i32),
+        }
+
+    def struct(self, fields) -> _lib.PbgWindowOut:
+        o = _lib.PbgWindowOut()
+        for k in fields:
+            setattr(o, k, _ptr(self.t[k]))
+        return o
+
+
+class HotPath:
+    """call kernel (pileup -> rows) + window-statistics kernel (rows -> per-window stats)."""
+
+    def __init__(self, ctx: _lib.Context, synth: SynthPileup, windows, stats: int, min_freq: int = 1,
+                 device: str = "cuda"):
+        self.ctx, self.synth, self.stats = ctx, synth, stats
+        self.rows = torch.zeros(synth.n_sites * ctx.row_bytes, dtype=torch.uint8, device=device)
+        w = torch.tensor([x for ab in windows for x in ab], dtype=torch.int32)
+        self.wins = w.to(device)
+        self.n_win = len(windows)
+        p = ctx.params
+        self.out = WindowOutputs(self.n_win, p.n_samples, p.n_pops, device)
+        fields = ["num_sites", "segsites"]
+        if stats & _lib.PBG_S_NUCDIV:
+            fields += ["pi", "dxy"]
+        if stats & _lib.PBG_S_SFS:
+            fields += ["td", "fwh"]
+        if stats & (_lib.PBG_S_ZNS | _lib.PBG_S_OMEGA | _lib.PBG_S_WALL):
+            fields += ["ld_snps", "ld_val", "ld_q"]
+        if stats & _lib.PBG_S_DIV_IND:
+            fields += ["div_ind"]
+        if stats & _lib.PBG_S_DIV_POP:
+            fields += ["div_fixed", "div_seg", "div_pop"]
+        if stats & (_lib.PBG_S_HAP_K | _lib.PBG_S_HAP_EHHS | _lib.PBG_S_HAP_DXY):
+            fields += ["nhaps", "hap_val", "hap_dxy", "hap_min"]
+        self.out_struct = self.out.struct(fields)
+        self.opts = _lib.PbgStatOpts(stats, min_freq, 0, 0)
+        self.pl = synth.pileup()
+
+    def call(self, stream=None, cb: torch.Tensor | None = None):
+        s = stream_handle(stream)
+        self.ctx.check(self.ctx.lib.pbg_call_sites(self.ctx.h, C.byref(self.pl), _ptr(self.rows),
+                                                   _ptr(cb) if cb is not None else None, s), "pbg_call_sites")
+
+    def window_stats(self, stream=None):
+        s = stream_handle(stream)
+        self.ctx.check(self.ctx.lib.pbg_window_stats(self.ctx.h, _ptr(self.rows), self.synth.n_sites, _ptr(self.wins),
+                                                     self.n_win, C.byref(self.opts), C.byref(self.out_struct), s),
+                       "pbg_window_stats")
+
+    def step(self, stream=None):
+        self.call(stream)
+        self.window_stats(stream)

@@ -1,0 +1,258 @@
+"""Shared test harness: option/region/sample setup for a golden case, plus the ctypes
+binding of the CPU oracle (oracle/liboracle.so -- test infrastructure, the checker)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+
+from popbam_amd import options as opt  # noqa: E402
+import fixtures  # noqa: E402
+
+ORACLE_SO = os.path.join(REPO, "oracle", "liboracle.so")
+
+
+class OrcParams(C.Structure):
+    _fields_ = [("n_samples", C.c_int32), ("n_pops", C.c_int32), ("pop_mask", C.c_uint64 * 64),
+                ("pop_n", C.c_int32 * 64), ("min_depth", C.c_int32), ("max_depth", C.c_int32),
+                ("min_rmsQ", C.c_int32), ("min_snpQ", C.c_int32), ("min_mapQ", C.c_int32),
+                ("min_baseQ", C.c_int32), ("flag", C.c_uint32)]
+
+
+class OrcCmd(C.Structure):
+    _fields_ = [("cmd", C.c_int32), ("output", C.c_int32), ("min_sites", C.c_int32), ("min_snps", C.c_int32),
+                ("min_freq", C.c_int32), ("outidx", C.c_int32), ("jc", C.c_int32), ("windowed", C.c_int32),
+                ("win_size", C.c_int64), ("beg", C.c_int32), ("end", C.c_int32), ("chr_name", C.c_char_p),
+                ("sample_names", C.POINTER(C.c_char_p)), ("pop_names", C.POINTER(C.c_char_p))]
+
+
+_orc = None
+
+
+def oracle():
+    global _orc
+    if _orc is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "oracle"], check=True,
+                           capture_output=True)
+        lib = C.CDLL(ORACLE_SO)
+        P = C.POINTER
+        lib.orc_run.restype = C.c_long
+        lib.orc_run.argtypes = [P(OrcParams), P(OrcCmd), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                C.c_char_p, C.c_size_t]
+        lib.orc_call_sites.restype = C.c_int
+        lib.orc_call_sites.argtypes = [P(OrcParams), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.orc_windows_from_sites.restype = C.c_long
+        lib.orc_windows_from_sites.argtypes = [P(OrcParams), P(OrcCmd), C.c_void_p, C.c_void_p, C.c_uint32,
+                                               C.c_void_p, C.c_void_p, C.c_char_p, C.c_size_t]
+        lib.orc_synth_site.restype = None
+        lib.orc_synth_site.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p]
+        for nm in ("orc_fk", "orc_beta", "orc_lhet"):
+            getattr(lib, nm).restype = P(C.c_double)
+        _orc = lib
+    return _orc
+
+
+class Setup:
+    """Everything a run of `popbam <cmd> ... in.bam <region>` needs, derived exactly as the
+    reference derives it."""
+
+    def __init__(self, case_name, args, region):
+        self.case = fixtures.load_case(case_name)
+        self.opts = opt.parse_args(args[0], list(args[1:]) + ["in.bam", region])
+        o = self.opts
+        names = [r[0] for r in self.case["refs"]]
+        lens = [r[1] for r in self.case["refs"]]
+        self.tid, self.beg, self.end = opt.parse_region(o.region, names, lens)
+        self.sm = opt.parse_header(self.case["header"], "in.bam")
+        self.masks, self.pop_n = self.sm.pop_masks()
+        self.outidx = 0
+        if o.flag & opt.BAM_OUTGROUP:
+            self.outidx = max(i for i, s in enumerate(self.sm.samples) if s == o.outgroup)
+        self.chr = names[self.tid]
+        self.batch = fixtures.case_batch(case_name, o.max_depth)
+
+    def orc_params(self):
+        o = self.opts
+        p = OrcParams()
+        p.n_samples, p.n_pops = self.sm.n, len(self.sm.pops)
+        for i, (m, c) in enumerate(zip(self.masks, self.pop_n)):
+            p.pop_mask[i], p.pop_n[i] = m, c
+        p.min_depth, p.max_depth, p.min_rmsQ, p.min_snpQ = o.min_depth, o.max_depth, o.min_rmsQ, o.min_snpQ
+        p.min_mapQ, p.min_baseQ, p.flag = o.min_mapQ & 0xFF, o.min_baseQ & 0xFF, o.flag
+        return p
+
+    def orc_cmd(self):
+        o = self.opts
+        c = OrcCmd()
+        c.cmd = opt.CMD_IDS[o.cmd]
+        c.output = o.output
+        c.min_sites = o.min_sites
+        c.min_snps = o.min_snps
+        c.min_freq = o.min_freq
+        c.outidx = self.outidx
+        c.jc = 1 if o.dist == "jc" else 0
+        c.windowed = 1 if o.flag & opt.BAM_WINDOW else 0
+        c.win_size = o.win_size
+        c.beg, c.end = self.beg, self.end
+        self._keep = [self.chr.encode()] + [s.encode() for s in self.sm.samples] + [p.encode() for p in self.sm.pops]
+        c.chr_name = self._keep[0]
+        sn = (C.c_char_p * max(1, self.sm.n))(*[s.encode() for s in self.sm.samples])
+        pn = (C.c_char_p * max(1, len(self.sm.pops)))(*[p.encode() for p in self.sm.pops])
+        self._arrs = (sn, pn)
+        c.sample_names = C.cast(sn, C.POINTER(C.c_char_p))
+        c.pop_names = C.cast(pn, C.POINTER(C.c_char_p))
+        return c
+
+
+def oracle_run(setup: Setup) -> str:
+    lib = oracle()
+    b = setup.batch
+    p, c = setup.orc_params(), setup.orc_cmd()
+    ref = np.ascontiguousarray(b["ref"])
+    dep = np.ascontiguousarray(b["depth"])
+    rd = np.ascontiguousarray(b["reads"]) if len(b["reads"]) else np.zeros(1, np.uint32)
+    cap = 1 << 20
+    while True:
+        buf = C.create_string_buffer(cap)
+        r = lib.orc_run(C.byref(p), C.byref(c), len(ref), ref.ctypes.data, dep.ctypes.data, rd.ctypes.data, buf, cap)
+        if r >= 0:
+            return buf.value.decode()
+        if r == -1:
+            raise RuntimeError("orc_run failed")
+        cap = -r + 16
+
+
+def all_cases():
+    out = []
+    for name in fixtures.case_dirs():
+        meta = fixtures.load_case(name)["meta"]
+        for i, cs in enumerate(meta["cases"]):
+            out.append((name, i))
+    return out
+
+
+def same_output(args, golden: str, ours: str, oob_cells=None):
+    """Exact text equality, except snp -o 0 base cells where the reference read iupac[]
+    out of bounds (undefined behaviour): the oracle prints '?' there, and for other outputs
+    the cells the oracle marked (`oob_cells`) match anything.
+    Returns (ok, first differing (golden, ours) line pair)."""
+    if args[0] != "snp":
+        if golden == ours:
+            return True, None
+    gl, ol = golden.splitlines(), ours.splitlines()
+    if len(gl) != len(ol):
+        return False, (f"{len(gl)} lines", f"{len(ol)} lines")
+    oob_ok = args[0] == "snp"
+    oob_cells = oob_cells or set()
+    for li, (a, b) in enumerate(zip(gl, ol)):
+        if a == b:
+            continue
+        fa, fb = a.split("\t"), b.split("\t")
+        if oob_ok and len(fa) == len(fb) and all(
+                x == y or y == "?" or (li, j) in oob_cells for j, (x, y) in enumerate(zip(fa, fb))):
+            continue
+        return False, (a, b)
+    return True, None
+
+
+def snp_oob_cells(oracle_text: str):
+    """(line, column) of cells the oracle marked '?' (reference UB)."""
+    out = set()
+    for i, line in enumerate(oracle_text.splitlines()):
+        for j, f in enumerate(line.split("\t")):
+            if f == "?":
+                out.add((i, j))
+    return out
+
+
+def synth_batch(seed, pos_lo, pos_hi, n, mean_depth):
+    """Regenerate positions [pos_lo, pos_hi) of the synthetic pileup on the CPU (oracle copy
+    of the generator) as a dense host batch."""
+    lib = oracle()
+    L = pos_hi - pos_lo
+    ref = np.zeros(L, np.uint8)
+    dep = np.zeros((L, n), np.uint16)
+    buf = np.zeros(n * 2 * mean_depth + 1, np.uint32)
+    parts = []
+    r = np.zeros(1, np.uint8)
+    nr = np.zeros(1, np.uint32)
+    for i in range(L):
+        lib.orc_synth_site(seed, pos_lo + i, n, mean_depth, r.ctypes.data, dep[i].ctypes.data, buf.ctypes.data,
+                           nr.ctypes.data)
+        ref[i] = r[0]
+        parts.append(buf[:nr[0]].copy())
+    reads = np.concatenate(parts) if parts else np.zeros(0, np.uint32)
+    return dict(ref=ref, depth=dep, reads=reads)
+
+
+def oracle_params_from(pbg_params):
+    p = OrcParams()
+    p.n_samples, p.n_pops = pbg_params.n_samples, pbg_params.n_pops
+    for i in range(pbg_params.n_pops):
+        p.pop_mask[i], p.pop_n[i] = pbg_params.pop_mask[i], pbg_params.pop_n[i]
+    p.min_depth, p.max_depth = pbg_params.min_depth, pbg_params.max_depth
+    p.min_rmsQ, p.min_snpQ = pbg_params.min_rmsQ, pbg_params.min_snpQ
+    p.min_mapQ, p.min_baseQ, p.flag = pbg_params.min_mapQ, pbg_params.min_baseQ, pbg_params.flag
+    return p
+
+
+def oracle_call(p, batch):
+    """orc_call_sites over a host batch -> (cb[L,n], types[L], fq[L], flags[L])."""
+    lib = oracle()
+    L, n = batch["depth"].shape
+    cb = np.zeros((L, n), np.uint64)
+    types = np.zeros(L, np.uint64)
+    fq = np.zeros(L, np.int16)
+    flags = np.zeros(L, np.uint8)
+    rd = batch["reads"] if len(batch["reads"]) else np.zeros(1, np.uint32)
+    assert lib.orc_call_sites(C.byref(p), L, np.ascontiguousarray(batch["ref"]).ctypes.data,
+                              np.ascontiguousarray(batch["depth"]).ctypes.data, np.ascontiguousarray(rd).ctypes.data,
+                              cb.ctypes.data, types.ctypes.data, fq.ctypes.data, flags.ctypes.data) == 0
+    return cb, types, fq, flags
+
+
+def rows_from_oracle(types, flags, row_bytes):
+    """Pack oracle per-position results into the product row format (include/popbam_gpu.h)."""
+    L = len(types)
+    counted = (flags & 2) > 0
+    seg = (flags & 4) > 0
+    if row_bytes == 16:
+        out = np.zeros((L, 2), np.uint64)
+        out[:, 0] = np.where(counted, types, 0)
+        out[:, 1] = np.where(counted, (np.uint64(1) << np.uint64(62)) |
+                             np.where(seg, np.uint64(1) << np.uint64(63), np.uint64(0)), 0)
+        return out.view(np.uint8).reshape(-1)
+    W = row_bytes * 8
+    v = types.astype(np.uint64) | (np.uint64(1) << np.uint64(W - 2)) | \
+        np.where(seg, np.uint64(1) << np.uint64(W - 1), np.uint64(0)).astype(np.uint64)
+    v = np.where(counted, v, np.uint64(0)).astype(np.uint64)
+    dt = {2: np.uint16, 4: np.uint32, 8: np.uint64}[row_bytes]
+    return v.astype(dt).view(np.uint8)
+
+
+def rows_to_sites(rows_u8, row_bytes, n_sites):
+    """Unpack product rows -> (types u64, flags u8 with bit1 counted, bit2 seg)."""
+    if row_bytes == 16:
+        w = rows_u8.view(np.uint64).reshape(n_sites, 2)
+        types, hi = w[:, 0], w[:, 1]
+        counted = (hi >> np.uint64(62)) & np.uint64(1)
+        seg = (hi >> np.uint64(63)) & np.uint64(1)
+    else:
+        dt = {2: np.uint16, 4: np.uint32, 8: np.uint64}[row_bytes]
+        v = rows_u8.view(dt).astype(np.uint64)
+        W = row_bytes * 8
+        counted = (v >> np.uint64(W - 2)) & np.uint64(1)
+        seg = (v >> np.uint64(W - 1)) & np.uint64(1)
+        types = v & ((np.uint64(1) << np.uint64(W - 2)) - np.uint64(1)) if W < 64 else v & np.uint64(0x3FFFFFFFFFFFFFFF)
+    flags = (counted.astype(np.uint8) << 1) | (seg.astype(np.uint8) << 2)
+    return types.astype(np.uint64), flags.astype(np.uint8)

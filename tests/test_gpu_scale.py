@@ -1,0 +1,171 @@
+"""GPU parity with the CPU oracle on the HBM-resident synthetic workload (beyond fixture
+sizes): the generator, the call kernel for every row width (2/4/8/16-byte rows), and the
+window-statistics kernel for every statistic, on LDS-resident and workspace-resident
+windows, overlapping windows, and > 65535 pairwise differences (u16 wrap)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import harness
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0xC0FFEE02
+
+
+def _ctx(n, **kw):
+    from popbam_amd import _lib, workload
+    params = workload.default_params(n, **kw)
+    return _lib.Context(params, 0), params
+
+
+def test_synthetic_generator_matches_oracle(gpu_lib):
+    import torch
+    from popbam_amd import workload
+    ctx, params = _ctx(12)
+    syn = workload.SynthPileup(ctx, 64 * 4000, 10, SEED)
+    depth = syn.depth.cpu().numpy().view(np.uint16).reshape(-1, 12)
+    boff = syn.block_off.cpu().numpy()
+    reads = syn.reads.cpu().numpy().view(np.uint32)
+    ref = syn.ref.cpu().numpy()
+    rng = np.random.default_rng(1)
+    for b in rng.choice(4000, 12, replace=False):
+        lo, hi = int(b) * 64, int(b) * 64 + 64
+        cpu = harness.synth_batch(SEED, lo, hi, 12, 10)
+        assert np.array_equal(ref[lo:hi], cpu["ref"])
+        assert np.array_equal(depth[lo:hi], cpu["depth"])
+        assert np.array_equal(reads[boff[b]:boff[b + 1]], cpu["reads"])
+    assert boff[-1] == syn.n_reads == int(depth.astype(np.int64).sum())
+    ctx.close()
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n,kw", [
+    (12, {}),                                   # 2-byte rows (the benchmark shape)
+    (11, {"min_snpQ": 40}),                     # more low-quality reverts (segbase borrow)
+    (24, {}),                                   # 4-byte rows
+    (24, {"flag": 0x02}),                       # Illumina 1.3+ qualities (-i)
+    (40, {"min_baseQ": 30, "min_mapQ": 61}),    # every read filtered by mapQ: k = 0 path
+    (62, {}),                                   # 8-byte rows, widest single word
+    (64, {"max_depth": 12, "min_depth": 8}),    # 16-byte rows, depth filters
+    (12, {"flag": 0x20}),                       # BAM_HETEROZYGOTE: heterozygotes kept
+])
+def test_call_kernel_matches_oracle(gpu_lib, n, kw):
+    import torch
+    from popbam_amd import workload
+    ctx, params = _ctx(n, **kw)
+    n_sites = 64 * max(60, 24000 // n)
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + n)
+    hp = workload.HotPath(ctx, syn, [(0, n_sites)], 0)
+    cb = torch.zeros(n_sites * n, dtype=torch.int64, device="cuda")
+    hp.call(cb=cb)
+    torch.cuda.synchronize()
+    rows = hp.rows.cpu().numpy()
+    cbh = cb.cpu().numpy().view(np.uint64).reshape(n_sites, n)
+    batch = harness.synth_batch(SEED + n, 0, n_sites, n, 10)
+    ocb, types, fq, flags = harness.oracle_call(harness.oracle_params_from(params), batch)
+    bad = np.nonzero((cbh != ocb).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} positions differ, first {bad[0]}: gpu {cbh[bad[0]]} oracle {ocb[bad[0]]}"
+    assert np.array_equal(rows, harness.rows_from_oracle(types, flags, ctx.row_bytes))
+    ctx.close()
+
+
+def _window_text(ctx, params, hp, cmd_id, output, windows, min_freq=1, jc=0, min_snps=10, flag_sub=False):
+    """Format the GPU window outputs with the library's print_<stat> (pbg_format)."""
+    from popbam_amd import _lib
+    n, np_ = params.n_samples, params.n_pops
+    host = {k: v.cpu().numpy() for k, v in hp.out.t.items()}
+    o = _lib.PbgWindowOut()
+    for k in [f for f, _ in _lib.PbgWindowOut._fields_]:
+        setattr(o, k, host[k].ctypes.data)
+    c = _lib.PbgCmd()
+    c.cmd, c.output, c.min_sites, c.min_snps, c.min_freq, c.jc = cmd_id, output, 10, min_snps, min_freq, jc
+    c.chr_name = b"chr1"
+    sn = (C.c_char_p * n)(*[f"s{i}".encode() for i in range(n)])
+    pn = (C.c_char_p * np_)(*[f"p{i}".encode() for i in range(np_)])
+    c.sample_names = C.cast(sn, C.POINTER(C.c_char_p))
+    c.pop_names = C.cast(pn, C.POINTER(C.c_char_p))
+    wb = np.array([a for a, _ in windows], np.int32)
+    we = np.array([b for _, b in windows], np.int32)
+    cap = 1 << 24
+    buf = C.create_string_buffer(cap)
+    need = C.c_size_t()
+    r = ctx.lib.pbg_format(ctx.h, C.byref(c), C.byref(o), len(windows), wb.ctypes.data, we.ctypes.data, buf, cap,
+                           C.byref(need))
+    ctx.check(r, "pbg_format")
+    return buf.value.decode()
+
+
+def _oracle_text(params, types, flags, cmd_id, output, windows, min_freq=1, jc=0, min_snps=10):
+    p = harness.oracle_params_from(params)
+    c = harness.OrcCmd()
+    n, np_ = params.n_samples, params.n_pops
+    c.cmd, c.output, c.min_sites, c.min_snps, c.min_freq, c.jc = cmd_id, output, 10, min_snps, min_freq, jc
+    c.chr_name = b"chr1"
+    sn = (C.c_char_p * n)(*[f"s{i}".encode() for i in range(n)])
+    pn = (C.c_char_p * np_)(*[f"p{i}".encode() for i in range(np_)])
+    c.sample_names = C.cast(sn, C.POINTER(C.c_char_p))
+    c.pop_names = C.cast(pn, C.POINTER(C.c_char_p))
+    wb = np.array([a for a, _ in windows], np.int32)
+    we = np.array([b for _, b in windows], np.int32)
+    cap = 1 << 24
+    buf = C.create_string_buffer(cap)
+    r = harness.oracle().orc_windows_from_sites(C.byref(p), C.byref(c), types.ctypes.data, flags.ctypes.data,
+                                                len(windows), wb.ctypes.data, we.ctypes.data, buf, cap)
+    assert r >= 0
+    return buf.value.decode()
+
+
+STATS = [  # (PBG_S_* flag, popbam_func_t, -o, min_freq, jc)
+    (0x001, 4, 0, 1, 0), (0x002, 6, 0, 1, 0), (0x004, 5, 0, 1, 0), (0x004, 5, 0, 2, 0), (0x008, 5, 1, 1, 0),
+    (0x010, 5, 2, 1, 0), (0x020, 2, 0, 1, 0), (0x040, 2, 1, 1, 0), (0x080, 1, 0, 1, 0), (0x100, 1, 1, 1, 0),
+    (0x200, 1, 2, 1, 0),
+]
+
+
+@pytest.mark.parametrize("layout", ["ref10kb", "overlap", "ragged"])
+@pytest.mark.parametrize("stat,cmd_id,output,min_freq,jc", STATS)
+def test_window_stats_match_oracle(gpu_lib, layout, stat, cmd_id, output, min_freq, jc):
+    import torch
+    from popbam_amd import workload
+    n_sites = 64 * 8000 if stat != 0x008 else 64 * 1600      # omega_max is O(S^3) on the oracle
+    ctx, params = _ctx(12)
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED)
+    if layout == "ref10kb":
+        wins = workload.reference_windows(0, n_sites, 10_000)
+    elif layout == "overlap":
+        wins = [(s, s + 1000) for s in range(0, n_sites - 1000, 500)]           # 1 kb / 500 bp step
+    else:
+        rng = np.random.default_rng(7)
+        cuts = np.sort(rng.choice(n_sites, 40, replace=False))
+        wins = [(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])] + [(5, 5), (0, 1)]
+    hp = workload.HotPath(ctx, syn, wins, stat, min_freq=min_freq)
+    hp.opts.jc = jc
+    hp.step()
+    torch.cuda.synchronize()
+    types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites)
+    gpu = _window_text(ctx, params, hp, cmd_id, output, wins, min_freq, jc)
+    orc = _oracle_text(params, types, flags, cmd_id, output, wins, min_freq, jc)
+    assert gpu == orc
+    ctx.close()
+
+
+def test_u16_wrap_and_workspace_window(gpu_lib):
+    """One window over 1.28 M positions: ~25 k segregating sites (beyond LDS -> global
+    workspace) and > 65535 differences per pair for some pairs at high theta."""
+    import torch
+    from popbam_amd import _lib, workload
+    n_sites = 64 * 20000
+    ctx, params = _ctx(12)
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 99)
+    wins = [(0, n_sites), (1000, n_sites - 3)]
+    for stat, cmd_id, output in [(0x001, 4, 0), (0x200, 1, 2), (0x020, 2, 0), (0x002, 6, 0), (0x004, 5, 0)]:
+        hp = workload.HotPath(ctx, syn, wins, stat)
+        hp.step()
+        torch.cuda.synchronize()
+        types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites)
+        assert int((flags & 4 > 0).sum()) > _lib.PBG_MAX_SAMPLES * 32
+        assert _window_text(ctx, params, hp, cmd_id, output, wins) == _oracle_text(params, types, flags, cmd_id,
+                                                                                  output, wins)
+    ctx.close()
