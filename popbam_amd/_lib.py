@@ -70,6 +70,14 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                            "(there is no CPU fallback)")
+    # One HIP runtime per process: the PyTorch ROCm wheel bundles its own libamdhip64.so.7 /
+    # libhsa-runtime64.so.1 and loads them under different file names.  If this library
+    # pulled /opt/rocm's copies in first, torch would later load a second HSA runtime that
+    # finds no GPU.  Importing torch first makes our NEEDED sonames bind to its copies.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     P = C.POINTER
     vp = C.c_void_p

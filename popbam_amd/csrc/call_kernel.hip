@@ -42,20 +42,18 @@ __device__ __forceinline__ void cswap(uint32_t &a, uint32_t &b) {  // descending
     b = lo;
 }
 
-// 16-input sorting network (Green, 60 comparators), descending.
+// 16-input Batcher odd-even merge sorting network (63 comparators), descending.  Verified
+// exhaustively by the 0-1 principle in tests/test_kernel_source.py.
 __device__ __forceinline__ void sort16_desc(uint32_t *k) {
 #define CS(i, j) cswap(k[i], k[j])
-    CS(0, 1); CS(2, 3); CS(4, 5); CS(6, 7); CS(8, 9); CS(10, 11); CS(12, 13); CS(14, 15);
-    CS(0, 2); CS(1, 3); CS(4, 6); CS(5, 7); CS(8, 10); CS(9, 11); CS(12, 14); CS(13, 15);
-    CS(0, 4); CS(1, 5); CS(2, 6); CS(3, 7); CS(8, 12); CS(9, 13); CS(10, 14); CS(11, 15);
-    CS(0, 8); CS(1, 9); CS(2, 10); CS(3, 11); CS(4, 12); CS(5, 13); CS(6, 14); CS(7, 15);
-    CS(5, 10); CS(6, 9); CS(3, 12); CS(13, 14); CS(7, 11); CS(1, 2); CS(4, 8);
-    CS(1, 4); CS(7, 13); CS(2, 8); CS(11, 14); CS(5, 6); CS(9, 10);
-    CS(1, 2); CS(3, 5); CS(13, 14); CS(10, 12); CS(6, 9); CS(7, 11); CS(4, 8);
-    CS(2, 4); CS(11, 13); CS(3, 8); CS(7, 12);
-    CS(6, 8); CS(10, 12); CS(3, 5); CS(7, 9);
-    CS(3, 4); CS(5, 6); CS(7, 8); CS(9, 10); CS(11, 12);
-    CS(6, 7); CS(8, 9);
+    CS(0, 1); CS(2, 3); CS(0, 2); CS(1, 3); CS(1, 2); CS(4, 5); CS(6, 7); CS(4, 6);
+    CS(5, 7); CS(5, 6); CS(0, 4); CS(2, 6); CS(2, 4); CS(1, 5); CS(3, 7); CS(3, 5);
+    CS(1, 2); CS(3, 4); CS(5, 6); CS(8, 9); CS(10, 11); CS(8, 10); CS(9, 11); CS(9, 10);
+    CS(12, 13); CS(14, 15); CS(12, 14); CS(13, 15); CS(13, 14); CS(8, 12); CS(10, 14); CS(10, 12);
+    CS(9, 13); CS(11, 15); CS(11, 13); CS(9, 10); CS(11, 12); CS(13, 14); CS(0, 8); CS(4, 12);
+    CS(4, 8); CS(2, 10); CS(6, 14); CS(6, 10); CS(2, 4); CS(6, 8); CS(10, 12); CS(1, 9);
+    CS(5, 13); CS(5, 9); CS(3, 11); CS(7, 15); CS(7, 11); CS(3, 5); CS(7, 9); CS(11, 13);
+    CS(1, 2); CS(3, 4); CS(5, 6); CS(7, 8); CS(9, 10); CS(11, 12); CS(13, 14);
 #undef CS
 }
 
