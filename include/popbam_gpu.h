@@ -108,7 +108,8 @@ typedef struct { int32_t beg, end; } pbg_window;   /* row index range [beg, end)
 #define PBG_S_HAP_DXY  0x200   /* haplo -o 2            (pop_haplo.cpp:325-363)       */
 
 typedef struct {
-    uint32_t stats;        /* PBG_S_* mask                                                */
+    uint32_t stats;        /* PBG_S_* mask; at most one of ZNS / OMEGA / WALL (they share
+                              ld_snps / ld_val)                                            */
     int32_t  min_freq;     /* ld: 1, or 2 with -e                                         */
     int32_t  outidx;       /* sfs/diverge outgroup sample (-p) when PBG_F_OUTGROUP is set  */
     int32_t  jc;           /* diverge -d jc                                                */

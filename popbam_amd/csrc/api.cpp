@@ -35,7 +35,12 @@ struct pbg_ctx {
     uint32_t ws_nwin = 0, ws_nrows = 0, ws_stats = 0;
     bool ws_need = false;
     uint64_t *d_ws = nullptr, *d_wsoff = nullptr;
-    size_t ws_cap = 0, wsoff_cap = 0;
+    size_t ws_cap = 0, wsoff_cap = 0, segcnt_cap = 0;
+    int32_t *d_segcnt = nullptr;
+    // list of positions with a sample deeper than the register sort width (call kernel)
+    void *d_deep = nullptr;
+    uint32_t *d_ndeep = nullptr;
+    size_t deep_cap = 0;   // entries
 };
 
 namespace {
@@ -163,7 +168,8 @@ void pbg_destroy(pbg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
-                    (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff})
+                    (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, c->d_deep, (void *)c->d_ndeep,
+                    (void *)c->d_segcnt})
         if (p) (void)hipFree(p);
     delete c;
 }
@@ -190,8 +196,16 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         c->cap_sites = pl->n_sites;
     }
     const uint32_t cap = c->cap_val;
+    if (c->deep_cap < pl->n_sites) {   // worst case: every position deep
+        if (c->d_deep) HIPCHK(c, hipFree(c->d_deep));
+        c->d_deep = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_deep, (size_t)pl->n_sites * pbg::deep_site_bytes()));
+        c->deep_cap = pl->n_sites;
+    }
+    if (!c->d_ndeep) HIPCHK(c, hipMalloc((void **)&c->d_ndeep, sizeof(uint32_t)));
     HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, pl->n_sites, pl->ref, pl->depth, pl->block_off,
-                                     pl->reads, cap, rows, cb, c->d_err, (hipStream_t)stream));
+                                     pl->reads, cap, rows, cb, c->d_err, c->d_deep, c->d_ndeep,
+                                     (hipStream_t)stream));
     return PBG_OK;
 }
 
@@ -199,6 +213,10 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
                      const pbg_stat_opts *o, const pbg_window_out *out, void *stream) {
     if (!c || !rows || !wins || !o || !out) return fail(c, PBG_E_ARG, "null argument");
     if (n_win == 0) return PBG_OK;
+    {
+        const uint32_t ld = o->stats & (PBG_S_ZNS | PBG_S_OMEGA | PBG_S_WALL);
+        if (ld & (ld - 1)) return fail(c, PBG_E_ARG, "at most one of ZnS / omega / Wall per call (shared outputs)");
+    }
     HIPCHK(c, hipSetDevice(c->device));
     pbg::StatsArgs A{};
     A.stats = o->stats;
@@ -225,7 +243,7 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
             off[i] = tot;
             tot += pbg::ws_slice(len, c->dp.n, c->dp.npops);
         }
-        c->ws_need = (o->stats & (PBG_S_OMEGA | PBG_S_WALL)) || maxlen > pbg::kSegCap ||
+        c->ws_need = (o->stats & (PBG_S_ZNS | PBG_S_OMEGA | PBG_S_WALL)) || maxlen > pbg::kSegCap ||
                      (int64_t)c->dp.n * (maxlen / 64 + 1) > pbg::kPlaneCap;
         if (c->ws_need) {
             if (tot * 8 > c->ws_cap) {
@@ -240,6 +258,12 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
                 HIPCHK(c, hipMalloc(&c->d_wsoff, n_win * 8));
                 c->wsoff_cap = n_win * 8;
             }
+            if (n_win * 4 > c->segcnt_cap) {
+                if (c->d_segcnt) HIPCHK(c, hipFree(c->d_segcnt));
+                c->d_segcnt = nullptr;
+                HIPCHK(c, hipMalloc((void **)&c->d_segcnt, n_win * 4));
+                c->segcnt_cap = n_win * 4;
+            }
             HIPCHK(c, hipMemcpyAsync(c->d_wsoff, off.data(), n_win * 8, hipMemcpyHostToDevice, (hipStream_t)stream));
             HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
         }
@@ -251,6 +275,7 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     if (c->ws_need) {
         A.ws = c->d_ws;
         A.ws_off = c->d_wsoff;
+        A.seg_count = c->d_segcnt;
     }
     HIPCHK(c, pbg::launch_window_stats(c->row_bytes, c->dp, c->dt, rows, n_rows, n_win, A, (hipStream_t)stream));
     return PBG_OK;

@@ -9,7 +9,6 @@ namespace pbg {
 
 constexpr int kBlockThreads = 256;     // 4 wave64 per workgroup
 constexpr int kSiteBlock = PBG_SITE_BLOCK;
-constexpr int kFastKeys = 16;          // register sort-network width in the call kernel
 
 // Parameters passed by value to the kernels (kernarg segment).
 struct DevParams {
@@ -93,6 +92,7 @@ struct StatsArgs {
     const pbg_window *wins;
     const uint64_t *ws_off;          // per-window offset into ws (u64 units), for big windows
     uint64_t *ws;                    // global workspace
+    int32_t *seg_count;              // per-window segregating-site count (LD chains)
     pbg_window_out out;
 };
 
@@ -100,7 +100,8 @@ struct StatsArgs {
 hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, uint32_t n_sites,
                              const uint8_t *ref, const uint16_t *depth, const uint64_t *block_off,
                              const uint32_t *reads, uint32_t cap, void *rows, uint64_t *cb, int *err,
-                             hipStream_t stream);
+                             void *deep_buf, uint32_t *n_deep, hipStream_t stream);
+size_t deep_site_bytes();
 size_t call_sites_lds_bytes(int n, uint32_t cap);
 hipError_t launch_synth_depth(uint64_t seed, int mean_depth, int n, uint32_t n_sites, uint8_t *ref,
                               uint16_t *depth, uint64_t *block_tot, hipStream_t stream);

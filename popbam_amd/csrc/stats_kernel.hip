@@ -93,7 +93,8 @@ __global__ __launch_bounds__(kBlockThreads) void window_stats_kernel(DevParams P
     }
     __syncthreads();
     const int num_sites = s_ns, S = s_S;
-    uint64_t *seg = (S <= kSegCap) ? s_seg : (A.ws + A.ws_off[w]);
+    const bool ld_next = (A.stats & (PBG_S_ZNS | PBG_S_OMEGA | PBG_S_WALL)) != 0;
+    uint64_t *seg = (S <= kSegCap && !ld_next) ? s_seg : (A.ws + A.ws_off[w]);
 
     // ---- pass 2: ordered compaction of segregating rows (ballot + cross-wave prefix)
     {
@@ -209,132 +210,9 @@ __global__ __launch_bounds__(kBlockThreads) void window_stats_kernel(DevParams P
         if (O.fwh) O.fwh[(size_t)w * np + i] = fwh;
     }
 
-    // ---- ld ZnS (lane per population), pop_ld.cpp:201-252
-    if ((A.stats & PBG_S_ZNS) && tid >= 128 && tid < 128 + np) {
-        const int i = tid - 128;
-        const int nn = P.pop_n[i], np1 = nn + 1, mf = A.min_freq;
-        const uint64_t pm = P.pop_mask[i];
-        int ns = 0;
-        double zns = 0.0;
-        if (S >= 1) {
-            for (int j = 0; j < S - 1; j++) {
-                uint64_t t1 = seg[j] & pm;
-                unsigned m1 = pc(t1);
-                if ((int)m1 >= mf && (int)m1 <= nn - mf) {
-                    ++ns;
-                    for (int k = j + 1; k < S; k++) {
-                        uint64_t t2 = seg[k] & pm;
-                        unsigned m2 = pc(t2);
-                        if ((int)m2 >= mf && (int)m2 <= nn - mf) zns += r2lookup(T, i, np1, m1, m2, pc(t1 & t2));
-                    }
-                }
-            }
-            ++ns;
-            zns *= 2.0 / (ns * (ns - 1));
-        }
-        if (O.ld_snps) O.ld_snps[(size_t)w * np + i] = ns;
-        if (O.ld_val) O.ld_val[(size_t)w * np + i] = x86nan(zns);
-    }
-
-    // ---- ld omega_max (lane per population), pop_ld.cpp:254-373: r^2 entries are looked
-    // up on the fly from the compressed variable-site list (no S x S matrix)
-    if ((A.stats & PBG_S_OMEGA) && tid >= 128 && tid < 128 + np) {
-        const int i = tid - 128;
-        const int nn = P.pop_n[i], np1 = nn + 1, mf = A.min_freq;
-        const uint64_t pm = P.pop_mask[i];
-        int ns = 0;
-        double om = 0.0;
-        if (S >= 1) {
-            // variable sites among the first S-1 (count1 indices); the last segregating
-            // site gets a count2 index if variable (V total)
-            int V = 0;
-            for (int j = 0; j < S; j++) {
-                unsigned m = pc(seg[j] & pm);
-                if ((int)m >= mf && (int)m <= nn - mf) {
-                    if (j < S - 1) ++ns;
-                    ++V;
-                }
-            }
-            ++ns;
-            // r2(a,b), a<b, variable-site indices; 0 when either index >= V
-            // variable types into the workspace (ws slice after planes) or LDS scratch
-            uint64_t *vt = A.ws + A.ws_off[w] + ws_list_off(len, n) + (uint64_t)i * (uint64_t)(len + 1);
-            {
-                int c = 0;
-                for (int j = 0; j < S; j++) {
-                    uint64_t t = seg[j] & pm;
-                    unsigned m = pc(t);
-                    if ((int)m >= mf && (int)m <= nn - mf) vt[c++] = t;
-                }
-            }
-            auto r2 = [&](int a, int b) -> double {
-                if (a >= V || b >= V) return 0.0;
-                uint64_t ta = vt[a], tb = vt[b];
-                return r2lookup(T, i, np1, pc(ta), pc(tb), pc(ta & tb));
-            };
-            double sl = 0, sr = 0, sb = 0;
-            for (int ii = 1; ii < ns - 1; ii++) {
-                for (int k = 0; k < ii; k++)
-                    for (int m = k + 1; m <= ii; m++) sl += r2(k, m);
-                for (int k = ii + 1; k < ns; k++)
-                    for (int m = 0; m <= ii; m++) sb += r2(m, k);
-                for (int k = ii + 1; k < ns - 1; k++)
-                    for (int m = k + 1; m < ns; m++) sr += r2(k, m);
-                int left = ii + 1, right = ns - left;
-                double omega = (sl + sr) / (((left * (left - 1)) / 2.0) + ((right * (right - 1)) / 2.0));
-                omega *= left * right / sb;
-                om = omega > om ? omega : om;
-            }
-        }
-        if (O.ld_snps) O.ld_snps[(size_t)w * np + i] = ns;
-        if (O.ld_val) O.ld_val[(size_t)w * np + i] = x86nan(om);
-    }
-
-    // ---- Wall's B / Q (one lane; last_type shared across populations, A.9)
-    if ((A.stats & PBG_S_WALL) && tid == 192) {
-        int ns[PBG_MAX_POPS], cong[PBG_MAX_POPS], part[PBG_MAX_POPS], nu[PBG_MAX_POPS];
-        for (int j = 0; j < np; j++) ns[j] = cong[j] = part[j] = nu[j] = 0;
-        uint64_t *uniq = A.ws + A.ws_off[w] + ws_list_off(len, n);   // np slices of (len+1)
-        uint64_t last_type = 0;
-        if (S >= 1) {
-            for (int i = 0; i < S; i++)
-                for (int j = 0; j < np; j++) {
-                    uint64_t t = seg[i];
-                    uint64_t type = t & P.pop_mask[j];
-                    uint64_t comp = ~t & P.pop_mask[j];
-                    uint64_t *u = uniq + (uint64_t)j * (uint64_t)(len + 1);
-                    if (type > 0 && type < P.pop_mask[j]) {
-                        if (ns[j] == 0) {
-                            u[nu[j]++] = type;
-                            last_type = type;
-                            ns[j]++;
-                        } else {
-                            if (type == last_type || comp == last_type) {
-                                cong[j]++;
-                                bool seen = false;
-                                for (int q = 0; q < nu[j]; q++) seen |= (u[q] == type) || (u[q] == comp);
-                                if (!seen) {
-                                    u[nu[j]++] = type;
-                                    part[j]++;
-                                }
-                            }
-                            ns[j]++;
-                            last_type = type;
-                        }
-                    }
-                }
-        }
-        for (int j = 0; j < np; j++) {
-            double b = 0.0, q = 0.0;
-            if (S >= 1) {
-                b = (double)cong[j] / (double)(ns[j] - 1);
-                q = (double)(cong[j] + part[j]) / ns[j];
-            }
-            if (O.ld_snps) O.ld_snps[(size_t)w * np + j] = ns[j];
-            if (O.ld_val) O.ld_val[(size_t)w * np + j] = x86nan(b);
-            if (O.ld_q) O.ld_q[(size_t)w * np + j] = x86nan(q);
-        }
-    }
+    // ZnS / omega_max / Wall's B,Q are serial chains per (window, population): they run in
+    // window_ld_kernel, one lane per chain, over the segregating lists left in the workspace.
+    if (tid == 0 && A.seg_count) A.seg_count[w] = S;
 
     // ---- diverge -o 0 (lane per sample): u16 accumulation of derived counts
     if ((A.stats & PBG_S_DIV_IND) && tid < n) {
@@ -454,6 +332,138 @@ __global__ __launch_bounds__(kBlockThreads) void window_stats_kernel(DevParams P
     }
 }
 
+
+// Serial LD chains, one lane per chain (pop_ld.cpp:201-458), reading the ordered segregating
+// lists window_stats_kernel compacted into the workspace.  Lanes of a wave belong to
+// different windows, so the dependent double additions of 64 chains overlap.
+__global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A) {
+    __shared__ double s_r2[4096];
+    const int n = P.n, np = P.npops;
+    int r2_total = 0;
+    for (int i = 0; i < np; ++i) r2_total += (P.pop_n[i] + 1) * (P.pop_n[i] + 1) * (P.pop_n[i] + 1);
+    const bool r2_lds = r2_total <= 4096;
+    if (r2_lds)
+        for (int i = threadIdx.x; i < r2_total; i += kBlockThreads) s_r2[i] = T.r2[i];
+    __syncthreads();
+    const double *r2tab = r2_lds ? s_r2 : T.r2;
+    const pbg_window_out &O = A.out;
+    const uint32_t gid = blockIdx.x * kBlockThreads + threadIdx.x;
+    if (A.stats & PBG_S_WALL) {
+        // one chain per window: last_type is shared by all populations (Appendix A.9)
+        const uint32_t w = gid;
+        if (w >= n_win) return;
+        const int64_t len = A.wins[w].end > A.wins[w].beg ? A.wins[w].end - A.wins[w].beg : 0;
+        const int S = A.seg_count[w];
+        const uint64_t *seg = A.ws + A.ws_off[w];
+        int ns[PBG_MAX_POPS], cong[PBG_MAX_POPS], part[PBG_MAX_POPS], nu[PBG_MAX_POPS];
+        for (int j = 0; j < np; j++) ns[j] = cong[j] = part[j] = nu[j] = 0;
+        uint64_t *uniq = A.ws + A.ws_off[w] + ws_list_off(len, n);   // np slices of (len+1)
+        uint64_t last_type = 0;
+        for (int i = 0; i < S; i++) {
+            const uint64_t t = seg[i];
+            for (int j = 0; j < np; j++) {
+                const uint64_t type = t & P.pop_mask[j];
+                const uint64_t comp = ~t & P.pop_mask[j];
+                uint64_t *u = uniq + (uint64_t)j * (uint64_t)(len + 1);
+                if (type > 0 && type < P.pop_mask[j]) {
+                    if (ns[j] == 0) {
+                        u[nu[j]++] = type;
+                        last_type = type;
+                        ns[j]++;
+                    } else {
+                        if (type == last_type || comp == last_type) {
+                            cong[j]++;
+                            bool seen = false;
+                            for (int q = 0; q < nu[j]; q++) seen |= (u[q] == type) || (u[q] == comp);
+                            if (!seen) {
+                                u[nu[j]++] = type;
+                                part[j]++;
+                            }
+                        }
+                        ns[j]++;
+                        last_type = type;
+                    }
+                }
+            }
+        }
+        for (int j = 0; j < np; j++) {
+            double b = 0.0, q = 0.0;
+            if (S >= 1) {
+                b = (double)cong[j] / (double)(ns[j] - 1);
+                q = (double)(cong[j] + part[j]) / ns[j];
+            }
+            if (O.ld_snps) O.ld_snps[(size_t)w * np + j] = ns[j];
+            if (O.ld_val) O.ld_val[(size_t)w * np + j] = x86nan(b);
+            if (O.ld_q) O.ld_q[(size_t)w * np + j] = x86nan(q);
+        }
+        return;
+    }
+    if (gid >= n_win * (uint32_t)np) return;
+    const uint32_t w = gid / np;
+    const int i = (int)(gid - w * np);
+    const int64_t len = A.wins[w].end > A.wins[w].beg ? A.wins[w].end - A.wins[w].beg : 0;
+    const int S = A.seg_count[w];
+    const uint64_t *seg = A.ws + A.ws_off[w];
+    const int nn = P.pop_n[i], np1 = nn + 1, mf = A.min_freq;
+    const uint64_t pm = P.pop_mask[i];
+    const double *r2p = r2tab + T.r2_off[i];
+    auto variable = [&](unsigned m) { return (int)m >= mf && (int)m <= nn - mf; };
+    int ns = 0;
+    double val = 0.0;
+    if (A.stats & PBG_S_ZNS) {   // calc_zns pop_ld.cpp:201-252
+        if (S >= 1) {
+            for (int j = 0; j < S - 1; j++) {
+                const uint64_t t1 = seg[j] & pm;
+                const unsigned m1 = pc(t1);
+                if (!variable(m1)) continue;
+                ++ns;
+                const double *row = r2p + (int)m1 * np1 * np1;
+#pragma unroll 4
+                for (int k = j + 1; k < S; k++) {
+                    const uint64_t t2 = seg[k] & pm;
+                    const unsigned m2 = pc(t2);
+                    if (variable(m2)) val += row[(int)m2 * np1 + (int)pc(t1 & t2)];
+                }
+            }
+            ++ns;
+            val *= 2.0 / (ns * (ns - 1));
+        }
+    } else {   // calc_omegamax pop_ld.cpp:254-373 (sums accumulate across partitions, A.8)
+        if (S >= 1) {
+            int V = 0;
+            uint64_t *vt = A.ws + A.ws_off[w] + ws_list_off(len, n) + (uint64_t)i * (uint64_t)(len + 1);
+            for (int j = 0; j < S; j++) {
+                const uint64_t t = seg[j] & pm;
+                if (variable(pc(t))) {
+                    if (j < S - 1) ++ns;
+                    vt[V++] = t;
+                }
+            }
+            ++ns;
+            auto r2 = [&](int a, int b) -> double {   // a < b; 0 beyond the variable sites
+                if (b >= V) return 0.0;
+                const uint64_t ta = vt[a], tb = vt[b];
+                return r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
+            };
+            double sl = 0, sr = 0, sb = 0;
+            for (int ii = 1; ii < ns - 1; ii++) {
+                for (int k = 0; k < ii; k++)
+                    for (int m = k + 1; m <= ii; m++) sl += r2(k, m);
+                for (int k = ii + 1; k < ns; k++)
+                    for (int m = 0; m <= ii; m++) sb += r2(m, k);
+                for (int k = ii + 1; k < ns - 1; k++)
+                    for (int m = k + 1; m < ns; m++) sr += r2(k, m);
+                const int left = ii + 1, right = ns - left;
+                double omega = (sl + sr) / (((left * (left - 1)) / 2.0) + ((right * (right - 1)) / 2.0));
+                omega *= left * right / sb;
+                val = omega > val ? omega : val;
+            }
+        }
+    }
+    if (O.ld_snps) O.ld_snps[(size_t)w * np + i] = ns;
+    if (O.ld_val) O.ld_val[(size_t)w * np + i] = x86nan(val);
+}
+
 template __global__ void window_stats_kernel<2>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
 template __global__ void window_stats_kernel<4>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
 template __global__ void window_stats_kernel<8>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
@@ -472,6 +482,13 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
         case 4: hipLaunchKernelGGL(window_stats_kernel<4>, g, b, 0, stream, P, T, rows, n_rows, n_win, A); break;
         case 8: hipLaunchKernelGGL(window_stats_kernel<8>, g, b, 0, stream, P, T, rows, n_rows, n_win, A); break;
         default: hipLaunchKernelGGL(window_stats_kernel<16>, g, b, 0, stream, P, T, rows, n_rows, n_win, A); break;
+    }
+    const uint32_t ld = A.stats & (PBG_S_ZNS | PBG_S_OMEGA | PBG_S_WALL);
+    if (ld) {
+        if (ld != PBG_S_ZNS && ld != PBG_S_OMEGA && ld != PBG_S_WALL) return hipErrorInvalidValue;
+        const uint32_t chains = (ld == PBG_S_WALL) ? n_win : n_win * (uint32_t)P.npops;
+        hipLaunchKernelGGL(window_ld_kernel, dim3((chains + kBlockThreads - 1) / kBlockThreads), b, 0, stream, P, T,
+                           n_win, A);
     }
     return hipGetLastError();
 }
