@@ -81,3 +81,19 @@ def run_command(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, en
     finally:
         if own:
             ctx.close()
+
+
+def run_command_sharded(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, end: int, batch: dict,
+                        pos0: int = 0, device: int = 0, group=None) -> str | None:
+    """run_command over this rank's block of windows (popbam_amd.shard), on this rank's GPU,
+    with the TSV gathered to rank 0.  Each rank uploads only the positions its windows read."""
+    from . import shard
+    windowed = bool(o.flag & opt.BAM_WINDOW)
+
+    def block(b, e):
+        lo, hi = shard.positions_needed(b, e, o.win_size, windowed)
+        hi = max(hi, lo + 1)
+        sub = shard.slice_batch(batch, pos0, lo, hi)
+        return run_command(o, sm, chr_name, b, e, sub, pos0=sub["pos0"], device=device)
+
+    return shard.run_sharded(block, beg, end, o.win_size, windowed, group)
