@@ -1,0 +1,77 @@
+/* popbam_feed.h -- C-ABI of the host pileup feeder (libpopbam_feed.so).
+ *
+ * The host side of the drop-in boundary: reads BGZF/BAM + BAI +
+ * FASTA and walks the pileup of a region exactly as the reference's callback sees it,
+ * producing the dense batch that pbg_run / pbg_call_sites take (include/popbam_gpu.h).
+ * It replaces, for the hot path:
+ *   - bgzf.c (block reader), bam.c bam_read1 / bam_calend, bam_index.c bam_fetch
+ *     (bam_index.c:943-980: reads overlapping [beg, end) in file order);
+ *   - bam_pileup.c bam_plp_push / bam_plp_next / resolve_cigar2 (bam_pileup.c:90-407):
+ *     a position gets a callback iff at least one buffered read spans it; reads in push
+ *     (file) order; BAM_DEF_MASK (bam.h:123) and the 8000-read maxcnt (bam_pileup.c:375);
+ *   - the per-sample partition at the top of popbamData::call_base (popbam.cpp:220-249):
+ *     skip is_del / is_refskip / BAM_FUNMAP, skip reads without RG, RG -> sample (unknown RG
+ *     falls back to the file-name sample, else the reference's fatal error), first
+ *     max_depth reads per sample in pileup order;
+ *   - faidx.c fai_fetch of one contig (faidx.c:291; .fai used when present).
+ * Host memory only; no GPU.  Functions return 0 / a non-negative value on success and a
+ * negative PBF_E* code on error (message in pbf_last_error()); nothing exits.
+ */
+#ifndef POPBAM_FEED_H
+#define POPBAM_FEED_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBF_OK       0
+#define PBF_E_IO    -1
+#define PBF_E_FORMAT -2
+#define PBF_E_ARG   -3
+#define PBF_E_RG    -4     /* read group not assigned to a sample (reference: fatal_error) */
+
+typedef struct pbf_bam pbf_bam;
+
+/* one pileup batch over contig positions [pos0, pos0 + n_sites), laid out as pbg_pileup
+ * (include/popbam_gpu.h): ref bit 7 = no callback at that position                        */
+typedef struct {
+    uint32_t  n_sites;
+    int32_t   pos0;
+    uint8_t  *ref;         /* [n_sites]                                                    */
+    uint16_t *depth;       /* [n_sites * n_samples]                                        */
+    uint64_t *block_off;   /* [n_sites/64 + 2] reads before each 64-position block         */
+    uint32_t *reads;       /* [n_reads] baseQ | mapQ<<8 | nt16<<16 | strand<<20            */
+    uint64_t  n_reads;
+} pbf_batch;
+
+const char *pbf_last_error(void);   /* thread-local */
+
+/* Opens a BAM file and, if present, its index (<path>.bai).  */
+int  pbf_open(pbf_bam **out, const char *bam_path);
+void pbf_close(pbf_bam *b);
+const char *pbf_header_text(const pbf_bam *b);
+int  pbf_n_refs(const pbf_bam *b);
+const char *pbf_ref_name(const pbf_bam *b, int tid);
+int64_t pbf_ref_len(const pbf_bam *b, int tid);
+int  pbf_has_index(const pbf_bam *b);
+
+/* Pileup of contig `tid` over [beg, end).  `refseq` is the contig sequence (at least `end`
+ * bytes).  Read groups: rg_ids[i] -> rg_sample[i]; reads whose RG is not listed go to
+ * `fallback_sample` (>= 0; the reference's file-name sample when the header has no @RG) or
+ * fail with PBF_E_RG (-1) when they contribute a base.  The batch's arrays are allocated by
+ * the library; release them with pbf_batch_free.                                          */
+int  pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refseq,
+                const char *const *rg_ids, const int32_t *rg_sample, int n_rg, int32_t fallback_sample,
+                int n_samples, int max_depth, pbf_batch *out);
+void pbf_batch_free(pbf_batch *batch);
+
+/* fai_fetch: the whole sequence of contig `name` (case preserved, line breaks removed).
+ * *seq is malloc'ed (NUL-terminated); free with pbf_free.                                 */
+int  pbf_fasta_fetch(const char *fa_path, const char *name, char **seq, int64_t *len);
+void pbf_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpopbam_gpu.so")
+LIB_PATH = os.environ.get("POPBAM_GPU_LIB") or os.path.join(HERE, "libpopbam_gpu.so")
 
 PBG_MAX_SAMPLES = 64
 PBG_MAX_POPS = 16

@@ -24,6 +24,7 @@ struct pbg_ctx {
     pbg::DevTables dt{};
     int row_bytes = 8;
     double *d_fk = nullptr, *d_beta = nullptr, *d_lhet = nullptr, *d_sfs = nullptr, *d_r2 = nullptr;
+    double *d_fbeta = nullptr;
     int *d_err = nullptr;
     std::string err;
     // per-pileup LDS staging capacity (keyed by block_off pointer and size), so repeated
@@ -37,10 +38,9 @@ struct pbg_ctx {
     uint64_t *d_ws = nullptr, *d_wsoff = nullptr;
     size_t ws_cap = 0, wsoff_cap = 0, segcnt_cap = 0;
     int32_t *d_segcnt = nullptr;
-    // list of positions with a sample deeper than the register sort width (call kernel)
-    void *d_deep = nullptr;
-    uint32_t *d_ndeep = nullptr;
-    size_t deep_cap = 0;   // entries
+    // samples deeper than the register sort width (call kernel): queues + parked info bytes
+    pbg::DeepBufs deep{};
+    size_t deep_sites_cap = 0, deep_info_cap = 0;
 };
 
 namespace {
@@ -132,6 +132,15 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     if ((e = upload(&c->d_fk, fk)) != hipSuccess) return bad(e, "upload fk");
     if ((e = upload(&c->d_beta, beta)) != hipSuccess) return bad(e, "upload beta");
     if ((e = upload(&c->d_lhet, lhet)) != hipSuccess) return bad(e, "upload lhet");
+    {
+        std::vector<double> fbeta(pbg::kFbetaSize, 0.0);
+        for (uint32_t q = 0; q < 64; ++q)
+            for (uint32_t nn = 0; nn < (uint32_t)pbg::kFbetaN; ++nn)
+                for (uint32_t cc = 0; cc < 16; ++cc)
+                    for (uint32_t w = 0; w < 16; ++w)
+                        fbeta[pbg::fbeta_index(q, nn, cc, w)] = fk[w] * beta[q << 16 | nn << 8 | cc];
+        if ((e = upload(&c->d_fbeta, fbeta)) != hipSuccess) return bad(e, "upload fbeta");
+    }
     // Tajima constants are indexed by population size and built for n = sm->n (pop_sfs.cpp:53-56)
     std::vector<double> a1, a2, e1, e2;
     pbg::build_sfs_constants(p->n_samples, a1, a2, e1, e2);
@@ -155,6 +164,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     c->dt.fk = c->d_fk;
     c->dt.beta = c->d_beta;
     c->dt.lhet = c->d_lhet;
+    c->dt.fbeta = c->d_fbeta;
     c->dt.a1 = c->d_sfs;
     c->dt.a2 = c->d_sfs + L;
     c->dt.e1 = c->d_sfs + 2 * L;
@@ -168,7 +178,8 @@ void pbg_destroy(pbg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
-                    (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, c->d_deep, (void *)c->d_ndeep,
+                    (void *)c->d_fbeta, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff,
+                    (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
                     (void *)c->d_segcnt})
         if (p) (void)hipFree(p);
     delete c;
@@ -187,25 +198,37 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         HIPCHK(c, hipMemcpyAsync(&total, pl->block_off + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost,
                                  (hipStream_t)stream));
         HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
-        const double mean = (double)total / nblk;
+        // reads staged per round = reads of kBlockThreads consecutive (position, sample) tasks
+        const double mean = (double)total / ((double)pl->n_sites * c->dp.n) * pbg::kBlockThreads;
         uint32_t cap = (uint32_t)(mean + 6.0 * std::sqrt(mean) + 64.0);
         cap = (cap + 63) & ~63u;
-        const uint32_t max_cap = (uint32_t)((64 * 1024 - pbg::call_sites_lds_bytes(c->dp.n, 0)) / 4);
+        const uint32_t max_cap = (uint32_t)((48 * 1024 - pbg::call_sites_lds_bytes(c->dp.n, 0)) / 4);
         c->cap_val = std::min(std::max(cap, 256u), max_cap);
         c->cap_key = pl->block_off;
         c->cap_sites = pl->n_sites;
     }
     const uint32_t cap = c->cap_val;
-    if (c->deep_cap < pl->n_sites) {   // worst case: every position deep
-        if (c->d_deep) HIPCHK(c, hipFree(c->d_deep));
-        c->d_deep = nullptr;
-        HIPCHK(c, hipMalloc(&c->d_deep, (size_t)pl->n_sites * pbg::deep_site_bytes()));
-        c->deep_cap = pl->n_sites;
+    // deep-sample queues: positions (worst case all), parked info bytes (n per position), and a
+    // task queue sized for ~3 % of tasks; overflowing tasks are computed inside the main kernel
+    if (c->deep_sites_cap < pl->n_sites || c->deep_info_cap < (size_t)pl->n_sites * c->dp.n) {
+        for (void *p : {(void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info})
+            if (p) HIPCHK(c, hipFree(p));
+        c->deep.sites = nullptr;
+        c->deep.tasks = nullptr;
+        c->deep.info = nullptr;
+        c->deep_sites_cap = c->deep_info_cap = 0;
+        const size_t ntask = (size_t)pl->n_sites * c->dp.n;
+        const size_t tcap = std::min<size_t>(ntask / 32 + 65536, 0xFFFFFFFFu);
+        HIPCHK(c, hipMalloc((void **)&c->deep.sites, (size_t)pl->n_sites * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc((void **)&c->deep.tasks, tcap * sizeof(pbg::DeepTask)));
+        HIPCHK(c, hipMalloc((void **)&c->deep.info, ntask));
+        c->deep.task_cap = (uint32_t)tcap;
+        c->deep_sites_cap = pl->n_sites;
+        c->deep_info_cap = ntask;
     }
-    if (!c->d_ndeep) HIPCHK(c, hipMalloc((void **)&c->d_ndeep, sizeof(uint32_t)));
+    if (!c->deep.count) HIPCHK(c, hipMalloc((void **)&c->deep.count, 2 * sizeof(uint32_t)));
     HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, pl->n_sites, pl->ref, pl->depth, pl->block_off,
-                                     pl->reads, cap, rows, cb, c->d_err, c->d_deep, c->d_ndeep,
-                                     (hipStream_t)stream));
+                                     pl->reads, cap, rows, cb, c->d_err, c->deep, (hipStream_t)stream));
     return PBG_OK;
 }
 

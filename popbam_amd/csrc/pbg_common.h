@@ -24,10 +24,20 @@ struct DevTables {
     const double *fk;     // [256]            fk[n]   (pop_utils.cpp:216-219)
     const double *beta;   // [64*256*256]     beta[q<<16|n<<8|k] (pop_utils.cpp:230-245)
     const double *lhet;   // [256*256]        lhet[n<<8|k] (pop_utils.cpp:248-251)
+    // fk[w] * beta[q<<16|n<<8|c] for the register path (n <= 16 keys, c, w < 16), indexed
+    // fbeta_index(q, n, c, w).  The product is the one IEEE double multiply errmod_cal does
+    // per key (pop_utils.cpp:311), so the table value is bit-identical to it.
+    const double *fbeta;  // [64*17*16*16]
     const double *a1, *a2, *e1, *e2;          // Tajima/Fay-Wu constants (pop_sfs.cpp:511-571)
     const double *r2;     // concatenated per-population r^2 tables, see r2_off
     int32_t r2_off[PBG_MAX_POPS];             // offset of population p's (n_p+1)^3 table
 };
+
+constexpr int kFbetaN = 17;   // n in [0, 16]
+__host__ __device__ inline uint32_t fbeta_index(uint32_t q, uint32_t n, uint32_t c, uint32_t w) {
+    return ((q * kFbetaN + n) << 8) | (c << 4) | w;
+}
+constexpr size_t kFbetaSize = 64u * kFbetaN * 256u;
 
 __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ULL;
@@ -96,12 +106,28 @@ struct StatsArgs {
     pbg_window_out out;
 };
 
+// Samples deeper than the register sort width (16 reads) are finished outside the main call
+// kernel: it queues them as tasks (lane-per-task kernel), parks the position's other per-sample
+// info bytes in `info` ([n_sites * n], written only for such positions) and queues the
+// position for a final fold.  A task that does not fit in the queue is computed in place.
+struct DeepTask {
+    uint32_t site;
+    uint32_t sd;        // sample | depth << 8
+    uint64_t off;       // index in reads[] of the task's first read
+};
+struct DeepBufs {
+    uint32_t *sites;    // [n_sites] positions with a queued task
+    DeepTask *tasks;    // [task_cap]
+    uint8_t *info;      // [n_sites * n]
+    uint32_t *count;    // [0] positions, [1] tasks (may exceed task_cap: overflow computed in place)
+    uint32_t task_cap;
+};
+
 // kernel launchers (defined in call_kernel.hip / stats_kernel.hip)
 hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, uint32_t n_sites,
                              const uint8_t *ref, const uint16_t *depth, const uint64_t *block_off,
                              const uint32_t *reads, uint32_t cap, void *rows, uint64_t *cb, int *err,
-                             void *deep_buf, uint32_t *n_deep, hipStream_t stream);
-size_t deep_site_bytes();
+                             const struct DeepBufs &D, hipStream_t stream);
 size_t call_sites_lds_bytes(int n, uint32_t cap);
 hipError_t launch_synth_depth(uint64_t seed, int mean_depth, int n, uint32_t n_sites, uint8_t *ref,
                               uint16_t *depth, uint64_t *block_tot, hipStream_t stream);

@@ -1,0 +1,133 @@
+"""ctypes binding of libpopbam_feed.so (include/popbam_feed.h): the host pileup feeder.
+
+`Bam(path).pileup(...)` returns the dense batch dict ({'ref', 'depth', 'reads', 'pos0'})
+that popbam_amd.engine.run_command hands to pbg_run.  No GPU is involved here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpopbam_feed.so")
+
+EXPORTS = ["pbf_last_error", "pbf_open", "pbf_close", "pbf_header_text", "pbf_n_refs", "pbf_ref_name",
+           "pbf_ref_len", "pbf_has_index", "pbf_pileup", "pbf_batch_free", "pbf_fasta_fetch", "pbf_free"]
+
+PBF_E_RG = -4
+
+
+class PbfBatch(C.Structure):
+    _fields_ = [("n_sites", C.c_uint32), ("pos0", C.c_int32), ("ref", C.POINTER(C.c_uint8)),
+                ("depth", C.POINTER(C.c_uint16)), ("block_off", C.POINTER(C.c_uint64)),
+                ("reads", C.POINTER(C.c_uint32)), ("n_reads", C.c_uint64)]
+
+
+class FeedError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build()")
+    lib = C.CDLL(LIB_PATH)
+    vp, P = C.c_void_p, C.POINTER
+    lib.pbf_last_error.restype = C.c_char_p
+    lib.pbf_open.argtypes = [P(vp), C.c_char_p]
+    lib.pbf_close.argtypes = [vp]
+    lib.pbf_close.restype = None
+    lib.pbf_header_text.argtypes = [vp]
+    lib.pbf_header_text.restype = C.c_char_p
+    lib.pbf_n_refs.argtypes = [vp]
+    lib.pbf_ref_name.argtypes = [vp, C.c_int]
+    lib.pbf_ref_name.restype = C.c_char_p
+    lib.pbf_ref_len.argtypes = [vp, C.c_int]
+    lib.pbf_ref_len.restype = C.c_int64
+    lib.pbf_has_index.argtypes = [vp]
+    lib.pbf_pileup.argtypes = [vp, C.c_int, C.c_int32, C.c_int32, C.c_char_p, P(C.c_char_p), P(C.c_int32),
+                               C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfBatch)]
+    lib.pbf_batch_free.argtypes = [P(PbfBatch)]
+    lib.pbf_batch_free.restype = None
+    lib.pbf_fasta_fetch.argtypes = [C.c_char_p, C.c_char_p, P(C.c_void_p), P(C.c_int64)]
+    lib.pbf_free.argtypes = [vp]
+    lib.pbf_free.restype = None
+    _lib = lib
+    return lib
+
+
+def _check(lib, rc):
+    if rc < 0:
+        raise FeedError(rc, lib.pbf_last_error().decode(errors="replace"))
+    return rc
+
+
+def fasta_fetch(path: str, name: str) -> bytes:
+    lib = load()
+    p = C.c_void_p()
+    n = C.c_int64()
+    _check(lib, lib.pbf_fasta_fetch(path.encode(), name.encode(), C.byref(p), C.byref(n)))
+    try:
+        return C.string_at(p, n.value)
+    finally:
+        lib.pbf_free(p)
+
+
+class Bam:
+    def __init__(self, path: str):
+        self.lib = load()
+        self.h = C.c_void_p()
+        _check(self.lib, self.lib.pbf_open(C.byref(self.h), path.encode()))
+        self.path = path
+
+    @property
+    def header_text(self) -> str:
+        return self.lib.pbf_header_text(self.h).decode(errors="replace")
+
+    @property
+    def refs(self):
+        return [(self.lib.pbf_ref_name(self.h, i).decode(), self.lib.pbf_ref_len(self.h, i))
+                for i in range(self.lib.pbf_n_refs(self.h))]
+
+    @property
+    def has_index(self) -> bool:
+        return bool(self.lib.pbf_has_index(self.h))
+
+    def pileup(self, tid: int, beg: int, end: int, refseq: bytes, rg2s: dict, n_samples: int, max_depth: int,
+               fallback_sample: int = -1) -> dict:
+        ids = list(rg2s)
+        rg = (C.c_char_p * max(1, len(ids)))(*[i.encode() for i in ids])
+        sm = (C.c_int32 * max(1, len(ids)))(*[rg2s[i] for i in ids])
+        if len(refseq) < end:
+            raise FeedError(-3, "reference sequence shorter than the region")
+        out = PbfBatch()
+        _check(self.lib, self.lib.pbf_pileup(self.h, tid, beg, end, refseq, rg, sm, len(ids), fallback_sample,
+                                             n_samples, max_depth, C.byref(out)))
+        try:
+            L = out.n_sites
+            ref = np.ctypeslib.as_array(out.ref, (max(L, 1),))[:L].copy()
+            depth = np.ctypeslib.as_array(out.depth, (max(L * n_samples, 1),))[:L * n_samples].copy()
+            reads = np.ctypeslib.as_array(out.reads, (max(out.n_reads, 1),))[:out.n_reads].copy()
+        finally:
+            self.lib.pbf_batch_free(C.byref(out))
+        return {"ref": ref, "depth": depth.reshape(L, n_samples), "reads": reads, "pos0": beg}
+
+    def close(self):
+        if self.h:
+            self.lib.pbf_close(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -42,3 +42,13 @@ def test_no_device_no_fallback():
     p.pop_mask[0], p.pop_n[0] = 3, 2
     h = C.c_void_p()
     assert lib.pbg_create(C.byref(h), 0, C.byref(p)) == _lib.PBG_E_NODEV
+
+
+def test_feeder_exports_header_symbols():
+    from popbam_amd import feed
+    txt = open(os.path.join(REPO, "include", "popbam_feed.h")).read()
+    names = sorted(set(re.findall(r"\b(pbf_[a-z_]+)\s*\(", txt)))
+    assert set(names) == set(feed.EXPORTS)
+    lib = feed.load()
+    for nm in names:
+        assert hasattr(lib, nm), nm
