@@ -1,10 +1,10 @@
 #!/bin/bash
 # Build an experimental variant of libpopbam_gpu.so with extra defines:
-#   bash tools_variant.sh NAME -DFOO=1 ...   ->  popbam_amd/variants/NAME/libpopbam_gpu.so
+#   bash tools/variant.sh NAME -DFOO=1 ...   ->  popbam_amd/variants/NAME/libpopbam_gpu.so
 # (git-ignored; load it with POPBAM_GPU_LIB=... for A/B timing on the GPU box)
 set -e
 NAME=$1; shift
-R=$(cd "$(dirname "$0")" && pwd)
+R=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$R/popbam_amd/variants/$NAME
 mkdir -p "$OUT/build"
 F="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function $*"
