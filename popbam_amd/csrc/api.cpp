@@ -138,7 +138,9 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
             for (uint32_t nn = 0; nn < (uint32_t)pbg::kFbetaN; ++nn)
                 for (uint32_t cc = 0; cc < 16; ++cc)
                     for (uint32_t w = 0; w < 16; ++w)
-                        fbeta[pbg::fbeta_index(q, nn, cc, w)] = fk[w] * beta[q << 16 | nn << 8 | cc];
+                        // q = 0 stays +0.0 (beta's q = 0 plane is never filled, pop_utils.cpp:230):
+                        // the register path relies on it for its zero padding words
+                        fbeta[pbg::fbeta_index(q, nn, cc, w)] = q ? fk[w] * beta[q << 16 | nn << 8 | cc] : 0.0;
         if ((e = upload(&c->d_fbeta, fbeta)) != hipSuccess) return bad(e, "upload fbeta");
     }
     // Tajima constants are indexed by population size and built for n = sm->n (pop_sfs.cpp:53-56)
