@@ -283,11 +283,13 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
                 HIPCHK(c, hipMalloc(&c->d_wsoff, n_win * 8));
                 c->wsoff_cap = n_win * 8;
             }
-            if (n_win * 4 > c->segcnt_cap) {
+            // seg_count [n_win] | var_count [n_win*np] | ld_ns [n_win*np]
+            const size_t segcnt_bytes = (size_t)n_win * (1 + 2 * (size_t)c->dp.npops) * 4;
+            if (segcnt_bytes > c->segcnt_cap) {
                 if (c->d_segcnt) HIPCHK(c, hipFree(c->d_segcnt));
                 c->d_segcnt = nullptr;
-                HIPCHK(c, hipMalloc((void **)&c->d_segcnt, n_win * 4));
-                c->segcnt_cap = n_win * 4;
+                HIPCHK(c, hipMalloc((void **)&c->d_segcnt, segcnt_bytes));
+                c->segcnt_cap = segcnt_bytes;
             }
             HIPCHK(c, hipMemcpyAsync(c->d_wsoff, off.data(), n_win * 8, hipMemcpyHostToDevice, (hipStream_t)stream));
             HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
@@ -301,6 +303,8 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
         A.ws = c->d_ws;
         A.ws_off = c->d_wsoff;
         A.seg_count = c->d_segcnt;
+        A.var_count = c->d_segcnt + n_win;
+        A.ld_ns = c->d_segcnt + n_win + (size_t)n_win * c->dp.npops;
     }
     HIPCHK(c, pbg::launch_window_stats(c->row_bytes, c->dp, c->dt, rows, n_rows, n_win, A, (hipStream_t)stream));
     return PBG_OK;

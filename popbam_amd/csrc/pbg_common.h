@@ -103,6 +103,8 @@ struct StatsArgs {
     const uint64_t *ws_off;          // per-window offset into ws (u64 units), for big windows
     uint64_t *ws;                    // global workspace
     int32_t *seg_count;              // per-window segregating-site count (LD chains)
+    int32_t *var_count;              // [n_win*npops] ZnS: rows variable within the population
+    int32_t *ld_ns;                  // [n_win*npops] ZnS: the reference's num_snps
     pbg_window_out out;
 };
 

@@ -214,6 +214,49 @@ __global__ __launch_bounds__(kBlockThreads) void window_stats_kernel(DevParams P
     // window_ld_kernel, one lane per chain, over the segregating lists left in the workspace.
     if (tid == 0 && A.seg_count) A.seg_count[w] = S;
 
+    // ---- ld -o 0 (ZnS, pop_ld.cpp:201-252): per population, the ordered list of segregating
+    // rows variable within it (masked to the population) for window_zns_kernel, and num_snps
+    // (variable sites among the first S-1, plus the final unconditional increment)
+    if ((A.stats & PBG_S_ZNS) && A.var_count) {
+        __shared__ int32_t s_lastvar;
+        for (int i = 0; i < np; ++i) {
+            const uint64_t pm = P.pop_mask[i];
+            const int nn = P.pop_n[i], mf = A.min_freq;
+            uint64_t *vl = A.ws + A.ws_off[w] + ws_list_off(len, n) + (uint64_t)i * (uint64_t)(len + 1);
+            int base = 0;
+            for (int c0 = 0; c0 < S; c0 += kBlockThreads) {
+                const int j = c0 + tid;
+                uint64_t t = 0;
+                bool v = false;
+                if (j < S) {
+                    t = seg[j] & pm;
+                    const int m = (int)pc(t);
+                    v = m >= mf && m <= nn - mf;
+                    if (j == S - 1) s_lastvar = v ? 1 : 0;
+                }
+                const uint64_t bm = __ballot(v);
+                const int before = (int)__popcll(bm & ((1ULL << lane) - 1));
+                __syncthreads();
+                if (lane == 0) s_wcnt[wv][0] = (uint32_t)__popcll(bm);
+                __syncthreads();
+                int wofs = 0, tot = 0;
+                for (int k = 0; k < kBlockThreads / 64; ++k) {
+                    if (k < wv) wofs += (int)s_wcnt[k][0];
+                    tot += (int)s_wcnt[k][0];
+                }
+                if (v) vl[base + wofs + before] = t;
+                base += tot;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                const int ns = S >= 1 ? base - s_lastvar + 1 : 0;
+                A.var_count[(size_t)w * np + i] = base;
+                A.ld_ns[(size_t)w * np + i] = ns;
+                if (A.out.ld_snps) A.out.ld_snps[(size_t)w * np + i] = ns;
+            }
+        }
+    }
+
     // ---- diverge -o 0 (lane per sample): u16 accumulation of derived counts
     if ((A.stats & PBG_S_DIV_IND) && tid < n) {
         uint32_t d = 0;
@@ -333,6 +376,121 @@ __global__ __launch_bounds__(kBlockThreads) void window_stats_kernel(DevParams P
 }
 
 
+// ZnS (calc_zns, pop_ld.cpp:201-252): per (window, population) chain, the sum of r^2 over
+// all pairs a < b of its variable sites in the reference's order (a ascending, then b), as
+// one dependent double add per pair.  A wave owns kZnsChains chains: all 64 lanes compute the
+// next 64 r^2 values of one row of one chain at a time (popcounts + r^2 table lookups),
+// writing them to LDS; then lane j adds chain j's values in order.  The parallel part is
+// spread over the wave, the serial part runs kZnsChains chains side by side.
+#ifndef PBG_ZNS_CHAINS
+#define PBG_ZNS_CHAINS 8
+#endif
+constexpr int kZnsChains = PBG_ZNS_CHAINS;
+constexpr int kZnsCap = 256;   // variable sites per chain staged in LDS (larger: read from HBM)
+
+__global__ __launch_bounds__(64) void window_zns_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A,
+                                                        int r2_lds) {
+    extern __shared__ double s_r2[];
+    __shared__ uint64_t s_t[kZnsChains][kZnsCap];
+    __shared__ double s_buf[kZnsChains][72];   // 64 values + zero tail for the groups of 8
+    const int lane = threadIdx.x, np = P.npops;
+    const uint32_t nch = n_win * (uint32_t)np;
+    const uint32_t c0 = blockIdx.x * kZnsChains;
+    for (int i = lane; i < r2_lds; i += 64) s_r2[i] = T.r2[i];
+    s_buf[lane >> 3][64 + (lane & 7)] = 0.0;
+
+    int Vc[kZnsChains], np1c[kZnsChains], offc[kZnsChains];
+    const uint64_t *Lg[kZnsChains];
+    int Vmax = 0;
+#pragma unroll
+    for (int j = 0; j < kZnsChains; ++j) {
+        const uint32_t ch = c0 + j;
+        Vc[j] = 0;
+        np1c[j] = 1;
+        offc[j] = 0;
+        Lg[j] = A.ws;
+        if (ch < nch) {
+            const uint32_t w = ch / (uint32_t)np;
+            const int i = (int)(ch - w * (uint32_t)np);
+            const int64_t len = A.wins[w].end > A.wins[w].beg ? A.wins[w].end - A.wins[w].beg : 0;
+            Vc[j] = A.var_count[ch];
+            np1c[j] = P.pop_n[i] + 1;
+            offc[j] = T.r2_off[i];
+            Lg[j] = A.ws + A.ws_off[w] + ws_list_off(len, P.n) + (uint64_t)i * (uint64_t)(len + 1);
+        }
+        Vmax = Vc[j] > Vmax ? Vc[j] : Vmax;
+    }
+    const bool fast = Vmax <= kZnsCap && r2_lds > 0;   // workgroup-uniform
+    if (fast) {
+#pragma unroll
+        for (int j = 0; j < kZnsChains; ++j)
+            for (int b = lane; b < Vc[j]; b += 64) s_t[j][b] = Lg[j][b];
+    }
+    __syncthreads();
+    // s_buf rows are zero-padded: adding +0.0 leaves a sum of r^2 values (>= +0) bit-unchanged,
+    // so each segment is summed in fixed groups of 8 whatever the chains' row lengths
+    double acc = 0.0;
+    for (int a = 0; a < Vmax - 1; ++a) {
+        for (int b0 = 0; b0 < Vmax - 1 - a; b0 += 64) {
+            if (fast) {   // straight-line over the chains: loads of all chains in flight together
+                uint64_t ta[kZnsChains], tb[kZnsChains];
+                bool ok[kZnsChains];
+#pragma unroll
+                for (int j = 0; j < kZnsChains; ++j) {
+                    const int L = Vc[j] - 1 - a;
+                    ok[j] = b0 + lane < L;
+                    const int ac = L > 0 ? a : 0, bc = ok[j] ? a + 1 + b0 + lane : 0;
+                    ta[j] = s_t[j][ac];
+                    tb[j] = s_t[j][bc];
+                    ta[j] = L > 0 ? ta[j] : 0;
+                    tb[j] = ok[j] ? tb[j] : 0;
+                }
+                double v[kZnsChains];
+#pragma unroll
+                for (int j = 0; j < kZnsChains; ++j) {
+                    const int np1 = np1c[j];
+                    v[j] = s_r2[offc[j] + ((int)pc(ta[j]) * np1 + (int)pc(tb[j])) * np1 + (int)pc(ta[j] & tb[j])];
+                }
+#pragma unroll
+                for (int j = 0; j < kZnsChains; ++j) s_buf[j][lane] = ok[j] ? v[j] : 0.0;
+            } else {      // a chain above kZnsCap, or r^2 tables too large for LDS: from HBM
+                for (int j = 0; j < kZnsChains; ++j) {
+                    const int L = Vc[j] - 1 - a;
+                    double v = 0.0;
+                    if (b0 + lane < L) {
+                        const uint64_t ta = Lg[j][a], tb = Lg[j][a + 1 + b0 + lane];
+                        const int np1 = np1c[j];
+                        v = T.r2[offc[j] + ((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
+                    }
+                    s_buf[j][lane] = v;
+                }
+            }
+            __syncthreads();
+            const int seg = min(64, Vmax - 1 - a - b0);   // longest segment of the wave's chains
+            if (lane < kZnsChains) {
+                for (int l = 0; l < seg; l += 8) {
+                    double x[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) x[u] = s_buf[lane][l + u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc += x[u];
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (lane < kZnsChains && c0 + lane < nch) {
+        const uint32_t ch = c0 + lane;
+        const uint32_t w = ch / (uint32_t)np;
+        double val = 0.0;
+        if (A.seg_count[w] >= 1) {
+            const int ns = A.ld_ns[ch];
+            val = acc * (2.0 / (ns * (ns - 1)));
+        }
+        if (A.out.ld_val) A.out.ld_val[ch] = x86nan(val);
+    }
+}
+
 // Serial LD chains, one lane per chain (pop_ld.cpp:201-458), reading the ordered segregating
 // lists window_stats_kernel compacted into the workspace.  Lanes of a wave belong to
 // different windows, so the dependent double additions of 64 chains overlap.
@@ -410,25 +568,7 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
     auto variable = [&](unsigned m) { return (int)m >= mf && (int)m <= nn - mf; };
     int ns = 0;
     double val = 0.0;
-    if (A.stats & PBG_S_ZNS) {   // calc_zns pop_ld.cpp:201-252
-        if (S >= 1) {
-            for (int j = 0; j < S - 1; j++) {
-                const uint64_t t1 = seg[j] & pm;
-                const unsigned m1 = pc(t1);
-                if (!variable(m1)) continue;
-                ++ns;
-                const double *row = r2p + (int)m1 * np1 * np1;
-#pragma unroll 4
-                for (int k = j + 1; k < S; k++) {
-                    const uint64_t t2 = seg[k] & pm;
-                    const unsigned m2 = pc(t2);
-                    if (variable(m2)) val += row[(int)m2 * np1 + (int)pc(t1 & t2)];
-                }
-            }
-            ++ns;
-            val *= 2.0 / (ns * (ns - 1));
-        }
-    } else {   // calc_omegamax pop_ld.cpp:254-373 (sums accumulate across partitions, A.8)
+    {   // calc_omegamax pop_ld.cpp:254-373 (ZnS runs in window_zns_kernel) (sums accumulate across partitions, A.8)
         if (S >= 1) {
             int V = 0;
             uint64_t *vt = A.ws + A.ws_off[w] + ws_list_off(len, n) + (uint64_t)i * (uint64_t)(len + 1);
@@ -487,8 +627,16 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
     if (ld) {
         if (ld != PBG_S_ZNS && ld != PBG_S_OMEGA && ld != PBG_S_WALL) return hipErrorInvalidValue;
         const uint32_t chains = (ld == PBG_S_WALL) ? n_win : n_win * (uint32_t)P.npops;
-        hipLaunchKernelGGL(window_ld_kernel, dim3((chains + kBlockThreads - 1) / kBlockThreads), b, 0, stream, P, T,
-                           n_win, A);
+        if (ld == PBG_S_ZNS) {
+            int r2_total = 0;
+            for (int i = 0; i < P.npops; ++i) r2_total += (P.pop_n[i] + 1) * (P.pop_n[i] + 1) * (P.pop_n[i] + 1);
+            const int r2_lds = r2_total <= 4096 ? r2_total : 0;
+            hipLaunchKernelGGL(window_zns_kernel, dim3((chains + kZnsChains - 1) / kZnsChains), dim3(64),
+                               (size_t)r2_lds * sizeof(double), stream, P, T, n_win, A, r2_lds);
+        } else {
+            hipLaunchKernelGGL(window_ld_kernel, dim3((chains + kBlockThreads - 1) / kBlockThreads), b, 0, stream, P,
+                               T, n_win, A);
+        }
     }
     return hipGetLastError();
 }
