@@ -121,9 +121,18 @@ struct DeepBufs {
     uint32_t *sites;    // [n_sites] positions with a queued task
     DeepTask *tasks;    // [task_cap]
     uint8_t *info;      // [n_sites * n]
-    uint32_t *count;    // [0] positions, [1] tasks (may exceed task_cap: overflow computed in place)
+    uint32_t *count;    // [0] positions, [1] tasks (may exceed task_cap: computed in place),
+                        // [2] rows-only pipeline: nonzero when a task was marked for the overflow kernel
     uint32_t task_cap;
+    // rows-only pipeline: block b owns tasks[b*blk_cap, (b+1)*blk_cap): tasks with at most 16
+    // reads from the start, deeper ones from the end; blk_cnt[b] = shallow | deep << 16
+    uint32_t *blk_cnt;
+    uint32_t blk_cap;
 };
+#ifndef PBG_QGROUP
+#define PBG_QGROUP 16
+#endif
+constexpr int kQueueGroup = PBG_QGROUP;   // blocks per wave in the queue kernels
 
 // kernel launchers (defined in call_kernel.hip / stats_kernel.hip)
 hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, uint32_t n_sites,

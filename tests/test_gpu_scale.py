@@ -71,6 +71,34 @@ def test_call_kernel_matches_oracle(gpu_lib, n, kw):
     ctx.close()
 
 
+@pytest.mark.parametrize("n,kw", [
+    (12, {}),                                   # the benchmark shape
+    (11, {"min_snpQ": 40}),
+    (24, {"flag": 0x02}),                       # Illumina offsets: fewer kept reads
+    (40, {"min_baseQ": 30, "min_mapQ": 61}),    # k = 0 everywhere: never reference-only
+    (64, {"max_depth": 12, "min_depth": 8}),
+    (12, {"flag": 0x20}),
+])
+def test_rows_only_call_matches_oracle(gpu_lib, n, kw):
+    """Rows without consensus words (the statistics path): the kernel may then skip the
+    likelihood of reference-only samples (class 0); the rows must still equal the oracle's."""
+    import torch
+    from popbam_amd import workload
+    ctx, params = _ctx(n, **kw)
+    n_sites = 64 * max(60, 24000 // n)
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 7 * n)
+    hp = workload.HotPath(ctx, syn, [(0, n_sites)], 0)
+    hp.call()
+    torch.cuda.synchronize()
+    rows = hp.rows.cpu().numpy()
+    batch = harness.synth_batch(SEED + 7 * n, 0, n_sites, n, 10)
+    _, types, _, flags = harness.oracle_call(harness.oracle_params_from(params), batch)
+    expect = harness.rows_from_oracle(types, flags, ctx.row_bytes)
+    bad = np.nonzero(rows != expect)[0] if rows.ndim == 1 else np.nonzero((rows != expect).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} rows differ, first at {bad[0]}"
+    ctx.close()
+
+
 def _window_text(ctx, params, hp, cmd_id, output, windows, min_freq=1, jc=0, min_snps=10, flag_sub=False):
     """Format the GPU window outputs with the library's print_<stat> (pbg_format)."""
     from popbam_amd import _lib
@@ -168,4 +196,69 @@ def test_u16_wrap_and_workspace_window(gpu_lib):
         assert int((flags & 4 > 0).sum()) > _lib.PBG_MAX_SAMPLES * 32
         assert _window_text(ctx, params, hp, cmd_id, output, wins) == _oracle_text(params, types, flags, cmd_id,
                                                                                   output, wins)
+    ctx.close()
+
+
+def _device_batch(batch, n):
+    import torch
+    ref = torch.from_numpy(np.ascontiguousarray(batch["ref"])).cuda()
+    dep = torch.from_numpy(np.ascontiguousarray(batch["depth"]).reshape(-1).view(np.int16)).cuda()
+    L = len(batch["ref"])
+    per_site = batch["depth"].astype(np.int64).sum(axis=1)
+    cum = np.concatenate([[0], np.cumsum(per_site)])
+    boff = torch.from_numpy(cum[::64].copy() if L % 64 == 0 else np.concatenate([cum[::64], cum[-1:]])).cuda()
+    rd = batch["reads"] if len(batch["reads"]) else np.zeros(1, np.uint32)
+    reads = torch.from_numpy(np.ascontiguousarray(rd).view(np.int32)).cuda()
+    return ref, dep, boff, reads
+
+
+@pytest.mark.parametrize("name", ["g01_base", "g05_lowdepth", "g06_softmask", "g07_multiallelic", "g08_filters",
+                                  "g10_deep"])
+def test_fixture_rows_only_and_cb_paths_match_oracle(gpu_lib, name):
+    """Both call pipelines (rows only: scan / queues / fold; with consensus words: the block
+    kernel) on the golden fixtures' pileups: every row equals the oracle's."""
+    import torch
+    import fixtures
+    from popbam_amd import _lib, engine
+    cs = fixtures.load_case(name)["meta"]["cases"][0]
+    st = harness.Setup(name, cs["args"], cs["region"])
+    params = engine.make_params(st.opts, st.sm)
+    ctx = _lib.Context(params, 0)
+    n = params.n_samples
+    ref, dep, boff, reads = _device_batch(st.batch, n)
+    L = len(st.batch["ref"])
+    pl = _lib.PbgPileup(L, 0, ref.data_ptr(), dep.data_ptr(), boff.data_ptr(), reads.data_ptr())
+    rb = ctx.row_bytes
+    _, types, _, flags = harness.oracle_call(harness.oracle_params_from(params), st.batch)
+    expect = harness.rows_from_oracle(types, flags, rb)
+    cbw = torch.zeros(L * n, dtype=torch.int64, device="cuda")
+    rows0 = torch.zeros(L * rb, dtype=torch.uint8, device="cuda")
+    ctx.check(ctx.lib.pbg_call_sites(ctx.h, C.byref(pl), rows0.data_ptr(), cbw.data_ptr(), None), "pbg_call_sites")
+    torch.cuda.synchronize()
+    cbh = cbw.cpu().numpy().view(np.uint64).reshape(L, n)
+    cum = np.concatenate([[0], np.cumsum(st.batch["depth"].reshape(-1).astype(np.int64))])
+
+    def detail(i):
+        out = []
+        for s_ in range(n):
+            t = i * n + s_
+            rr = st.batch["reads"][cum[t]:cum[t + 1]]
+            out.append((s_, int(cbh[i, s_] & 0xFFFF), [(int(r & 255), int((r >> 8) & 255), int((r >> 16) & 15))
+                                                       for r in rr]))
+        return out
+
+    for with_cb in (False, True):
+        rows = torch.zeros(L * rb, dtype=torch.uint8, device="cuda")
+        cb = torch.zeros(L * n, dtype=torch.int64, device="cuda") if with_cb else None
+        ctx.check(ctx.lib.pbg_call_sites(ctx.h, C.byref(pl), rows.data_ptr(), cb.data_ptr() if with_cb else None,
+                                         None), "pbg_call_sites")
+        torch.cuda.synchronize()
+        got = rows.cpu().numpy().reshape(L, rb)
+        exp = np.ascontiguousarray(expect).view(np.uint8).reshape(L, rb)
+        bad = np.nonzero((got != exp).any(axis=1))[0]
+        if bad.size:
+            i = int(bad[0])
+            msg = (f"cb={with_cb}: {bad.size} rows differ, first at {i}: gpu {got[i]} oracle {exp[i]} "
+                   f"ref {st.batch['ref'][i]} depth {st.batch['depth'][i].tolist()}\nbad {bad[:40].tolist()}\n{detail(i)}")
+            raise AssertionError(msg)
     ctx.close()
