@@ -182,7 +182,7 @@ void pbg_destroy(pbg_ctx *c) {
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
                     (void *)c->d_fbeta, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
-                    (void *)c->deep.blk_cnt,
+                    (void *)c->deep.blk_cnt, (void *)c->deep.raw,
                     (void *)c->d_segcnt})
         if (p) (void)hipFree(p);
     delete c;
@@ -214,9 +214,11 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
     // deep-sample queues: positions (worst case all), parked info bytes (n per position), and a
     // task queue sized for ~3 % of tasks; overflowing tasks are computed inside the main kernel
     if (c->deep_sites_cap < pl->n_sites || c->deep_info_cap < (size_t)pl->n_sites * c->dp.n) {
-        for (void *p : {(void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.blk_cnt})
+        for (void *p : {(void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.blk_cnt,
+                        (void *)c->deep.raw})
             if (p) HIPCHK(c, hipFree(p));
         c->deep.blk_cnt = nullptr;
+        c->deep.raw = nullptr;
         c->deep.sites = nullptr;
         c->deep.tasks = nullptr;
         c->deep.info = nullptr;
@@ -224,9 +226,10 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         const size_t ntask = (size_t)pl->n_sites * c->dp.n;
         const size_t nblk = (pl->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
         // rows-only calls queue every task that is not reference-only (~10 % at depth 10 with
-        // 1 % errors) in a per-block region of a quarter of the block's tasks (+32); the rest is
-        // computed by the overflow kernel.  The cb path's deep queue shares the array.
-        const uint32_t blk_cap = (uint32_t)(pbg::kSiteBlock * c->dp.n / 4 + 32);
+        // 1 % errors; segregating positions cluster them) in a per-block region of 3/16 of the
+        // block's tasks (+32); the rest is computed by the overflow kernel.  The cb path's deep
+        // queue shares the array.
+        const uint32_t blk_cap = (uint32_t)(pbg::kSiteBlock * c->dp.n * 3 / 16 + 32);
         const size_t tcap = std::max<size_t>(nblk * blk_cap, std::min<size_t>(ntask / 32 + 65536, 0xFFFFFFFFu));
         HIPCHK(c, hipMalloc((void **)&c->deep.sites, (size_t)pl->n_sites * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc((void **)&c->deep.tasks, tcap * sizeof(pbg::DeepTask)));
@@ -234,6 +237,7 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         c->deep.task_cap = (uint32_t)std::min<size_t>(tcap, 0xFFFFFFFFu);
         c->deep.blk_cap = blk_cap;
         HIPCHK(c, hipMalloc((void **)&c->deep.blk_cnt, nblk * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc((void **)&c->deep.raw, nblk * blk_cap * 4 * sizeof(uint4)));
         c->deep_sites_cap = pl->n_sites;
         c->deep_info_cap = ntask;
     }

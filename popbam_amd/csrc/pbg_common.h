@@ -128,6 +128,8 @@ struct DeepBufs {
     // reads from the start, deeper ones from the end; blk_cnt[b] = shallow | deep << 16
     uint32_t *blk_cnt;
     uint32_t blk_cap;
+    uint4 *raw;         // [nblk*blk_cap*4]: the reads of front (<= 16 reads) entries, copied by the
+                        // scan kernel from its LDS staging so the queue kernel loads them coalesced
 };
 #ifndef PBG_QGROUP
 #define PBG_QGROUP 16
