@@ -1,0 +1,71 @@
+"""The drop-in command line (popbam_amd/cli.py): `popbam <cmd> -f ref.fa [opts] in.bam region`
+read with the native feeder and computed on the GPU must print exactly what the compiled
+reference printed for every golden case (tests/golden/*/meta.json records the reference's
+argv: make_golden.py ran `popbam <cmd> -f ref.fa <args...> in.bam <region>`).  The error
+paths (fatal_error, pop_utils.cpp:510-519) need no GPU."""
+import os
+import shutil
+
+import pytest
+
+import fixtures
+import harness
+from popbam_amd import cli
+
+CASES = harness.all_cases()
+
+
+def _argv(name, cs):
+    d = fixtures.load_case(name)["dir"]
+    a = cs["args"]
+    return [a[0], "-f", os.path.join(d, "ref.fa")] + list(a[1:]) + [os.path.join(d, "in.bam"), cs["region"]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,idx", CASES, ids=[f"{n}-{i:02d}" for n, i in CASES])
+def test_cli_matches_reference(gpu_lib, name, idx):
+    cs = fixtures.load_case(name)["meta"]["cases"][idx]
+    argv = _argv(name, cs)
+    ours = cli.run(argv[0], argv[1:])
+    gold = fixtures.golden_text(name, cs["stdout"])
+    oob = None
+    if cs["args"][0] == "snp":
+        st = harness.Setup(name, cs["args"], cs["region"])
+        oob = harness.snp_oob_cells(harness.oracle_run(st))
+    ok, diff = harness.same_output(cs["args"], gold, ours, oob)
+    assert ok, f"{argv}\n gold: {diff[0]}\n ours: {diff[1]}"
+
+
+def _main(argv, capsys):
+    rc = cli.main(argv)
+    out = capsys.readouterr()
+    return rc, out.out, out.err
+
+
+def test_usage_and_unknown_commands(capsys):
+    rc, out, err = _main([], capsys)
+    assert rc == 1 and "Usage:" in err and out == ""
+    rc, out, err = _main(["frobnicate"], capsys)
+    assert rc == 1 and err == "Error: unrecognized command: frobnicate\n"
+    rc, out, err = _main(["tree", "x.bam", "chr1"], capsys)
+    assert rc == 1 and "tree" in err
+
+
+def test_fatal_errors_before_the_gpu(capsys, tmp_path):
+    d = fixtures.load_case("g01_base")["dir"]
+    ref, bam = os.path.join(d, "ref.fa"), os.path.join(d, "in.bam")
+    rc, out, err = _main(["nucdiv", "-f", ref, str(tmp_path / "missing.bam"), "chr1"], capsys)
+    assert rc == 1 and out == "" and err.startswith("popbam runtime error:\nCannot read BAM file")
+    assert err.endswith("Exiting program\n")
+    rc, out, err = _main(["nucdiv", "-f", ref, bam, "chrX:1-100"], capsys)
+    assert rc == 1 and "Bad genome coordinates: chrX:1-100" in err
+    rc, out, err = _main(["nucdiv", "-f", ref, bam], capsys)
+    assert rc == 1 and "Need to specify BAM file name" in err
+    rc, out, err = _main(["diverge", "-f", ref, "-d", "kimura", bam, "chr1"], capsys)
+    assert rc == 1 and "kimura is not a valid distance option" in err
+    noidx = tmp_path / "in.bam"
+    shutil.copy(bam, noidx)
+    rc, out, err = _main(["nucdiv", "-f", ref, str(noidx), "chr1"], capsys)
+    assert rc == 1 and f"Index file not available for BAM file {noidx}" in err
+    rc, out, err = _main(["nucdiv", "-f", str(tmp_path / "none.fa"), bam, "chr1"], capsys)
+    assert rc == 1 and "Failed to load index for fastA reference file" in err
