@@ -9,9 +9,10 @@ kernel over all 4,999 windows.  Multi-GPU: one process per GPU (torchrun), each 
 own 50 Msite shard (its own seed), no collective on the data path (weak scaling); only the
 timing barrier and max-over-ranks reduction use torch.distributed.
 
-Prints one JSON line (rank 0).  `roofline` is for the dominant kernel (the call kernel):
-algorithmic bytes per launch / its mean duration measured with HIP events on the stream the
-kernel runs on.  `cpu_baseline` times the CPU oracle (C++ restatement of the reference
+Prints one JSON line (rank 0).  `roofline` is for the dominant kernel (call_scan_kernel, the
+first kernel of the rows-only call): its algorithmic bytes per launch / its mean duration,
+measured with HIP events the library records on the stream the kernel runs on
+(pbg_set_kernel_timing / pbg_kernel_time).  `cpu_baseline` times the CPU oracle (C++ restatement of the reference
 path, one core) on a bounded sample of the same workload.
 """
 from __future__ import annotations
@@ -117,6 +118,9 @@ def main():
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events around the dominant kernel (call_scan_kernel), recorded by the library on the
+    # stream it launches on (torch's events only bracket whole stages)
+    ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 1), "pbg_set_kernel_timing")
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -138,15 +142,20 @@ def main():
 
     call_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
     stats_ms = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
+    kt, kn = C.c_double(0.0), C.c_uint32(0)
+    ctx.check(ctx.lib.pbg_kernel_time(ctx.h, C.byref(kt), C.byref(kn)), "pbg_kernel_time")
+    ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
+    scan_ms = kt.value / max(1, kn.value)
     total_sites = args.sites * world * args.steps
     value = total_sites / elapsed / 1e6
     call_bytes = syn.bytes_read_by_call()
-    achieved = call_bytes / (call_ms * 1e-3) / 1e9
+    scan_bytes = syn.bytes_scan_kernel()
+    achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
     stats_bytes = args.sites * ctx.row_bytes
 
     # per-launch HBM traffic from rocprofv3 PMC counters, when a profile of this code is committed
     traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_call_kernel.json")
+    pmc = os.path.join(REPO, "profiles", "pmc_call_scan_kernel.json")
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:
@@ -168,9 +177,12 @@ def main():
                        "sites_per_gpu": args.sites, "samples": n, "mean_depth": args.depth,
                        "window": args.window, "windows_per_gpu": len(wins), "reads_per_gpu": syn.n_reads,
                        "parallelism": f"dp{world} (independent window-range shards, no collective)"},
-            "roofline": {"bound": "hbm", "kernel": "call_sites_kernel", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": "call_scan_kernel", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "bytes_per_launch": call_bytes, "ms_per_launch": round(call_ms, 4)},
+                         "traffic": traffic, "bytes_per_launch": scan_bytes, "ms_per_launch": round(scan_ms, 4)},
+            "call_stage": {"ms_per_step": round(call_ms, 4), "bytes": call_bytes,
+                           "GBps": round(call_bytes / (call_ms * 1e-3) / 1e9, 2),
+                           "kernels": "call_scan + call_slow + call_deepq + call_overflow + call_fold"},
             "window_stats": {"ms_per_launch": round(stats_ms, 4), "rows_bytes": stats_bytes,
                              "GBps": round(stats_bytes / (stats_ms * 1e-3) / 1e9, 2),
                              "Msites_per_s_stats_only": round(args.sites / (stats_ms * 1e-3) / 1e6, 2)},

@@ -190,6 +190,15 @@ long pbg_run(pbg_ctx *ctx, const pbg_cmd *cmd, const pbg_pileup *host_pileup, ch
 long pbg_format(const pbg_ctx *ctx, const pbg_cmd *cmd, const pbg_window_out *host_out, uint32_t n_win,
                 const int32_t *wbeg, const int32_t *wend, char *out, size_t cap, size_t *needed);
 
+/* ---- profiling ---------------------------------------------------------------------- */
+/* With timing on, every pbg_call_sites records a pair of HIP events on its stream around its
+ * dominant kernel (the scan kernel of the rows-only pipeline, the block kernel when
+ * consensus words are requested); pbg_kernel_time waits for the recorded events and returns
+ * the summed elapsed milliseconds and the number of calls timed.  Turning timing on (again)
+ * restarts the count.  No reference counterpart (the reference has no timers).    */
+int pbg_set_kernel_timing(pbg_ctx *ctx, int on);
+int pbg_kernel_time(pbg_ctx *ctx, double *ms_total, uint32_t *launches);
+
 /* ---- synthetic workload (benchmark) ------------------------------------------------- */
 /* Counter-based pileup generator (splitmix64 keyed on (seed, position)), written straight
  * into device memory: pbg_synth_depth() fills ref/depth/block_off and reports the read

@@ -24,7 +24,8 @@ PBG_S_DIV_IND, PBG_S_DIV_POP, PBG_S_HAP_K, PBG_S_HAP_EHHS, PBG_S_HAP_DXY = 0x20,
 
 # every symbol include/popbam_gpu.h declares
 EXPORTS = ["pbg_create", "pbg_destroy", "pbg_last_error", "pbg_row_bytes", "pbg_device_count",
-           "pbg_call_sites", "pbg_window_stats", "pbg_run", "pbg_format", "pbg_synth_depth", "pbg_synth_reads"]
+           "pbg_call_sites", "pbg_window_stats", "pbg_run", "pbg_format", "pbg_set_kernel_timing",
+           "pbg_kernel_time", "pbg_synth_depth", "pbg_synth_reads"]
 
 
 class PbgParams(C.Structure):
@@ -100,6 +101,10 @@ def load():
     lib.pbg_format.argtypes = [vp, P(PbgCmd), P(PbgWindowOut), C.c_uint32, vp, vp, C.c_char_p, C.c_size_t,
                                P(C.c_size_t)]
     lib.pbg_format.restype = C.c_long
+    lib.pbg_set_kernel_timing.argtypes = [vp, C.c_int]
+    lib.pbg_set_kernel_timing.restype = C.c_int
+    lib.pbg_kernel_time.argtypes = [vp, P(C.c_double), P(C.c_uint32)]
+    lib.pbg_kernel_time.restype = C.c_int
     lib.pbg_synth_depth.argtypes = [vp, C.c_uint64, C.c_int32, C.c_uint32, vp, vp, vp, P(C.c_uint64), vp]
     lib.pbg_synth_depth.restype = C.c_int
     lib.pbg_synth_reads.argtypes = [vp, C.c_uint64, C.c_int32, C.c_uint32, vp, vp, vp, vp]

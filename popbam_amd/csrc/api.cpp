@@ -41,6 +41,10 @@ struct pbg_ctx {
     // samples deeper than the register sort width (call kernel): queues + parked info bytes
     pbg::DeepBufs deep{};
     size_t deep_sites_cap = 0, deep_info_cap = 0;
+    // pbg_set_kernel_timing: HIP events around the dominant call kernel of every call
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    size_t ev_used = 0;
 };
 
 namespace {
@@ -185,6 +189,10 @@ void pbg_destroy(pbg_ctx *c) {
                     (void *)c->deep.blk_cnt, (void *)c->deep.raw,
                     (void *)c->d_segcnt})
         if (p) (void)hipFree(p);
+    for (auto &e : c->ev) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
     delete c;
 }
 
@@ -242,8 +250,42 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         c->deep_info_cap = ntask;
     }
     if (!c->deep.count) HIPCHK(c, hipMalloc((void **)&c->deep.count, 4 * sizeof(uint32_t)));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing) {
+        if (c->ev_used == c->ev.size()) {
+            hipEvent_t a, b;
+            HIPCHK(c, hipEventCreate(&a));
+            HIPCHK(c, hipEventCreate(&b));
+            c->ev.emplace_back(a, b);
+        }
+        e0 = c->ev[c->ev_used].first;
+        e1 = c->ev[c->ev_used].second;
+        ++c->ev_used;
+    }
     HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, pl->n_sites, pl->ref, pl->depth, pl->block_off,
-                                     pl->reads, cap, rows, cb, c->d_err, c->deep, (hipStream_t)stream));
+                                     pl->reads, cap, rows, cb, c->d_err, c->deep, (hipStream_t)stream, e0, e1));
+    return PBG_OK;
+}
+
+int pbg_set_kernel_timing(pbg_ctx *c, int on) {
+    if (!c) return fail(c, PBG_E_ARG, "null argument");
+    c->timing = on != 0;
+    c->ev_used = 0;
+    return PBG_OK;
+}
+
+int pbg_kernel_time(pbg_ctx *c, double *ms_total, uint32_t *launches) {
+    if (!c || !ms_total || !launches) return fail(c, PBG_E_ARG, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    double tot = 0.0;
+    for (size_t i = 0; i < c->ev_used; ++i) {
+        HIPCHK(c, hipEventSynchronize(c->ev[i].second));
+        float ms = 0.0f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i].first, c->ev[i].second));
+        tot += ms;
+    }
+    *ms_total = tot;
+    *launches = (uint32_t)c->ev_used;
     return PBG_OK;
 }
 

@@ -140,7 +140,8 @@ constexpr int kQueueGroup = PBG_QGROUP;   // blocks per wave in the queue kernel
 hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, uint32_t n_sites,
                              const uint8_t *ref, const uint16_t *depth, const uint64_t *block_off,
                              const uint32_t *reads, uint32_t cap, void *rows, uint64_t *cb, int *err,
-                             const struct DeepBufs &D, hipStream_t stream);
+                             const struct DeepBufs &D, hipStream_t stream, hipEvent_t ev0 = nullptr,
+                             hipEvent_t ev1 = nullptr);
 size_t call_sites_lds_bytes(int n, uint32_t cap);
 hipError_t launch_synth_depth(uint64_t seed, int mean_depth, int n, uint32_t n_sites, uint8_t *ref,
                               uint16_t *depth, uint64_t *block_tot, hipStream_t stream);

@@ -66,13 +66,21 @@ class SynthPileup:
                               _ptr(self.reads))
 
     def bytes_read_by_call(self) -> int:
-        """Algorithmic HBM bytes one call-kernel launch must move: every read record (4 B),
-        the depth matrix (2 B per site x sample), the reference byte, the block offsets, and
-        the packed rows it writes."""
+        """Algorithmic HBM bytes of the call stage: every read record (4 B), the depth matrix
+        (2 B per site x sample), the reference byte, the block offsets, and the packed rows
+        it writes."""
         n = self.ctx.params.n_samples
         nblk = (self.n_sites + SITE_BLOCK - 1) // SITE_BLOCK
         return 4 * self.n_reads + 2 * self.n_sites * n + self.n_sites + 8 * (nblk + 1) + \
             self.ctx.row_bytes * self.n_sites
+
+    def bytes_scan_kernel(self) -> int:
+        """Algorithmic HBM bytes of one call_scan_kernel launch (the dominant kernel of the
+        rows-only call): every read record (4 B), the depths (2 B per site x sample), the
+        reference byte, the block offsets, and one info byte written per (site, sample)."""
+        n = self.ctx.params.n_samples
+        nblk = (self.n_sites + SITE_BLOCK - 1) // SITE_BLOCK
+        return 4 * self.n_reads + 2 * self.n_sites * n + self.n_sites + 8 * (nblk + 1) + self.n_sites * n
 
 
 def reference_windows(beg: int, end: int, win_size: int):

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Copy a GPU session's rocprofv3 results from gpurun_out/ into profiles/<tag>_* and derive
-the per-launch HBM traffic of the call kernel (profiles/pmc_call_kernel.json, read by bench.py).
+the per-launch HBM traffic of the dominant kernel (profiles/pmc_call_scan_kernel.json, read by bench.py).
 
 FETCH_SIZE on gfx950 reports half the bytes of wide coalesced streaming reads
 (MI355X_MICROARCH.md, HBM/rocprofv3 section): it is doubled here.  FETCH_SIZE and WRITE_SIZE
@@ -38,14 +38,14 @@ def main():
         f, w = fetch.get(k, 0.0), write.get(k, 0.0)
         lines.append(f"{k},{f:.3f},{int(f * 1024 * 2)},{w:.3f}")
     open(os.path.join(PROF, f"{tag}_pmc_hbm.csv"), "w").write("\n".join(lines) + "\n")
-    k = "call_sites_kernel"
+    k = b["roofline"]["kernel"]
     cfg = b["config"]
     pmc = {"kernel": k, "sites": cfg["sites_per_gpu"], "samples": cfg["samples"], "depth": cfg["mean_depth"],
            "fetch_size_kib": fetch[k], "write_size_kib": write[k], "fetch_correction": 2.0,
            "hbm_bytes_per_launch": int(fetch[k] * 1024 * 2 + write[k] * 1024),
            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on bench.py --steps 2, {tag}",
            "algorithmic_bytes_per_launch": b["roofline"]["bytes_per_launch"]}
-    json.dump(pmc, open(os.path.join(PROF, "pmc_call_kernel.json"), "w"), indent=1)
+    json.dump(pmc, open(os.path.join(PROF, f"pmc_{k}.json"), "w"), indent=1)
     print(json.dumps(pmc, indent=1))
 
 
