@@ -16,7 +16,7 @@ $H $F --offload-arch=gfx950 -c -o $OUT/build/stats.o $C/stats_kernel.hip &
 $H $F -x hip --offload-arch=gfx950 -c -o $OUT/build/api.o $C/api.cpp &
 $H $F -c -o $OUT/build/tables.o $C/host_tables.cpp &
 $H $F -c -o $OUT/build/format.o $C/format.cpp &
-wait
+wait || exit 1
 $H -shared -fPIC --offload-arch=gfx950 -o $OUT/libpopbam_gpu.so $OUT/build/*.o
 rm -rf "$OUT/build"
 echo "$OUT/libpopbam_gpu.so"
