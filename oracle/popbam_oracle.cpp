@@ -734,6 +734,56 @@ void do_snp(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
     }
 }
 
+// ---- snp -o 1: print_sweep pop_snp.cpp:243-268.  At a counted site every sample passes
+// qfilter, so pop_sample_mask = sample_cov & pop_mask = pop_mask.
+void do_sweep(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
+    for (int i = 0; i < W.segsites; i++) {
+        o.str(c->chr_name); o.str("\t"); o.i((long long)W.pos[i] + 1);
+        const uint64_t t = W.types[W.idx[i]];
+        for (int j = 0; j < p->n_pops; j++) {
+            const uint64_t pt = t & p->pop_mask[j];
+            const unsigned short pop_n = (unsigned short)popcnt64(p->pop_mask[j]);
+            unsigned short freq;
+            if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(pop_n - popcnt64(pt));
+            else freq = (unsigned short)popcnt64(pt);
+            o.str("\t"); o.i(freq); o.str("\t"); o.i(pop_n);
+        }
+        o.str("\n");
+    }
+}
+
+// ---- snp -o 2: print_ms pop_snp.cpp:270-303 (positions as std::setprecision(8) = %.8g)
+void do_ms(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
+    o.str("//\nsegsites: "); o.i(W.segsites); o.str("\npositions: ");
+    for (int i = 0; i < W.segsites; i++) {
+        char b[64];
+        std::snprintf(b, sizeof b, "%.8g ", (double)(unsigned)(W.pos[i] - (unsigned)W.beg) / (W.end - W.beg));
+        o.str(b);
+    }
+    o.str("\n");
+    for (int i = 0; i < p->n_samples; i++) {
+        for (int j = 0; j < W.segsites; j++) {
+            const bool d = (W.seq[i][j / 64] >> (j % 64)) & 1;
+            const bool flip = (p->flag & 0x40) && (W.types[W.idx[j]] >> c->outidx & 1);
+            o.str(d != flip ? "1" : "0");
+        }
+        o.str("\n");
+    }
+    o.str("\n");
+}
+
+// print_ms_header pop_snp.cpp:305-317, printed before the first window
+void ms_header(Out &o, const orc_params *p, long nwindows) {
+    o.str("ms "); o.i(p->n_samples); o.str(" "); o.i(nwindows);
+    if (p->n_pops > 1) {
+        o.str(" -t 5.0 -I "); o.i(p->n_pops); o.str(" ");
+        for (int i = 0; i < p->n_pops; i++) { o.i(p->pop_n[i]); o.str(" "); }
+    } else {
+        o.str(" -t 5.0 ");
+    }
+    o.str("\n1350154902\n\n");
+}
+
 struct SiteResult {
     std::vector<uint64_t> cb, types;
     std::vector<int16_t> fq;
@@ -815,7 +865,11 @@ void emit(Out &o, const orc_params *p, const orc_cmd *c, const Window &W, const 
         case ORC_LD: do_ld(o, p, c, W); break;
         case ORC_DIVERGE: do_diverge(o, p, c, W); break;
         case ORC_HAPLO: do_haplo(o, p, c, W); break;
-        case ORC_SNP: do_snp(o, p, c, W); break;
+        case ORC_SNP:
+            if (c->output == 1) do_sweep(o, p, c, W);
+            else if (c->output == 2) do_ms(o, p, c, W);
+            else do_snp(o, p, c, W);
+            break;
         default: break;
     }
 }
@@ -864,6 +918,7 @@ long orc_run(const orc_params *p, const orc_cmd *c, uint32_t n_sites, const uint
     SfsConst K = sfs_const(n);
     Out o;
     Window W;
+    if (c->cmd == ORC_SNP && c->output == 2) ms_header(o, p, num_windows);
     for (long cw = 0; cw < num_windows; cw++) {
         int wb, we;
         if (c->windowed) {  // "chr:beg+cw*w+1-(cw+1)*w+beg-1" through bam_parse_region

@@ -455,6 +455,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
     hipStream_t s = nullptr;
     const int rb = c->row_bytes;
     const bool is_snp = cmd->cmd == PBG_CMD_SNP;
+    const bool snp_words = is_snp && cmd->output == 0;   // only -o 0 prints consensus words
     if (dsites) {
         std::vector<uint64_t> lb(dblk + 1);
         for (uint32_t b = 0; b <= dblk; ++b) lb[b] = hboff[blo + b] - r0;
@@ -468,10 +469,10 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
                             hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(d_boff.p, lb.data(), (dblk + 1) * 8, hipMemcpyHostToDevice));
         if (r1 > r0) HIPCHK(c, hipMemcpy(d_reads.p, hp->reads + r0, (r1 - r0) * 4, hipMemcpyHostToDevice));
-        if (is_snp) HIPCHK(c, d_cb.alloc((size_t)dsites * n * 8));
+        if (snp_words) HIPCHK(c, d_cb.alloc((size_t)dsites * n * 8));
         pbg_pileup dp{dsites, (int32_t)dpos0, (const uint8_t *)d_ref.p, (const uint16_t *)d_dep.p,
                       (const uint64_t *)d_boff.p, (const uint32_t *)d_reads.p};
-        int rc = pbg_call_sites(c, &dp, d_rows.p, is_snp ? (uint64_t *)d_cb.p : nullptr, s);
+        int rc = pbg_call_sites(c, &dp, d_rows.p, snp_words ? (uint64_t *)d_cb.p : nullptr, s);
         if (rc) return rc;
         int herr = 0;
         HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
@@ -479,20 +480,38 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
     }
     std::string text;
     if (is_snp) {
-        // print_popbam_snp (pop_snp.cpp:224-241) per window: segregating positions in order
+        // print_snp per window (pop_snp.cpp:218-317): segregating positions in order, as
+        // print_popbam_snp (-o 0), print_sweep (-o 1) or print_ms (-o 2, header first)
+        if (cmd->output < 0 || cmd->output > 2) return fail(c, PBG_E_ARG, "snp output format must be 0, 1 or 2");
         std::vector<unsigned char> rows((size_t)dsites * rb);
-        std::vector<uint64_t> cb((size_t)dsites * n);
+        std::vector<uint64_t> cb(snp_words ? (size_t)dsites * n : 0);
         if (dsites) {
             HIPCHK(c, hipMemcpy(rows.data(), d_rows.p, rows.size(), hipMemcpyDeviceToHost));
-            HIPCHK(c, hipMemcpy(cb.data(), d_cb.p, cb.size() * 8, hipMemcpyDeviceToHost));
+            if (snp_words) HIPCHK(c, hipMemcpy(cb.data(), d_cb.p, cb.size() * 8, hipMemcpyDeviceToHost));
         }
-        for (auto &x : win)
+        const uint64_t tmask = n >= 64 ? ~0ULL : (1ULL << n) - 1;
+        if (cmd->output == 2) pbg::format_ms_header(text, n, np, c->params.pop_n, (long)win.size());
+        std::vector<int32_t> wpos;
+        std::vector<uint64_t> wtypes;
+        for (auto &x : win) {
+            wpos.clear();
+            wtypes.clear();
             for (int64_t p = std::max<int64_t>(x.first, dpos0); p < std::min<int64_t>(x.second, dpos0 + dsites); ++p) {
                 const size_t i = (size_t)(p - dpos0);
                 const unsigned char *r = rows.data() + i * rb;
-                const bool seg = (r[rb - 1] >> 7) & 1;
-                if (seg) pbg::format_snp_site(text, *cmd, n, (int32_t)p, hp->ref[p - pos0] & 0x7f, cb.data() + i * n);
+                if (!((r[rb - 1] >> 7) & 1)) continue;   // not segregating
+                uint64_t types = 0;
+                for (int b = 0; b < std::min(rb, 8); ++b) types |= (uint64_t)r[b] << (8 * b);
+                types &= tmask;
+                if (cmd->output == 0)
+                    pbg::format_snp_site(text, *cmd, n, (int32_t)p, hp->ref[p - pos0] & 0x7f, cb.data() + i * n);
+                else if (cmd->output == 1)
+                    pbg::format_sweep_site(text, *cmd, np, c->params.pop_mask, c->params.flag, (int32_t)p, types);
+                wpos.push_back((int32_t)p);
+                wtypes.push_back(types);
             }
+            if (cmd->output == 2) pbg::format_ms_window(text, n, c->params.flag, cmd->outidx, x.first, x.second, wpos, wtypes);
+        }
     } else {
         uint32_t stats = 0;
         switch (cmd->cmd) {

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "pbg_host.h"
 
@@ -176,6 +177,76 @@ void format_snp_site(std::string &out, const pbg_cmd &c, int n, int32_t pos, uns
         o.i((long long)((cb[j] >> 48) & 0xffff));
         o.t("\t");
         o.i((long long)((cb[j] >> 16) & 0xffff));
+    }
+    out += "\n";
+}
+
+// snp -o 1: print_sweep (pop_snp.cpp:243-268).  At a counted site every sample passes
+// qfilter, so the reference's pop_sample_mask (sample_cov & pop_mask) is pop_mask.
+void format_sweep_site(std::string &out, const pbg_cmd &c, int np, const uint64_t *pop_mask, uint32_t flag,
+                       int32_t pos, uint64_t types) {
+    W o{out};
+    o.t(c.chr_name);
+    o.t("\t");
+    o.i((long long)pos + 1);
+    for (int j = 0; j < np; j++) {
+        const uint64_t pt = types & pop_mask[j];
+        const unsigned pop_n = (unsigned)__builtin_popcountll(pop_mask[j]);
+        const bool flip = (flag & PBG_F_OUTGROUP) && ((types >> c.outidx) & 1);
+        const unsigned freq = (unsigned short)(flip ? pop_n - (unsigned)__builtin_popcountll(pt)
+                                                    : (unsigned)__builtin_popcountll(pt));
+        o.t("\t");
+        o.i(freq);
+        o.t("\t");
+        o.i(pop_n);
+    }
+    out += "\n";
+}
+
+// snp -o 2: print_ms_header (pop_snp.cpp:305-317), once before the first window
+void format_ms_header(std::string &out, int n, int np, const int32_t *pop_n, long nwindows) {
+    W o{out};
+    o.t("ms ");
+    o.i(n);
+    o.t(" ");
+    o.i(nwindows);
+    if (np > 1) {
+        o.t(" -t 5.0 -I ");
+        o.i(np);
+        o.t(" ");
+        for (int i = 0; i < np; i++) {
+            o.i(pop_n[i]);
+            o.t(" ");
+        }
+    } else {
+        o.t(" -t 5.0 ");
+    }
+    out += "\n1350154902\n\n";
+}
+
+// snp -o 2: print_ms (pop_snp.cpp:270-303) for one window [wbeg, wend): positions relative to
+// the window as std::setprecision(8) (printf "%.8g"), then one 0/1 string per sample, the
+// derived bit flipped where the outgroup carries it.
+void format_ms_window(std::string &out, int n, uint32_t flag, int outidx, int32_t wbeg, int32_t wend,
+                      const std::vector<int32_t> &pos, const std::vector<uint64_t> &types) {
+    W o{out};
+    const size_t S = pos.size();
+    o.t("//\nsegsites: ");
+    o.i((long long)S);
+    o.t("\npositions: ");
+    for (size_t i = 0; i < S; i++) {
+        char b[64];
+        std::snprintf(b, sizeof b, "%.8g ", (double)(unsigned)(pos[i] - wbeg) / (double)(wend - wbeg));
+        out += b;
+    }
+    out += "\n";
+    for (int i = 0; i < n; i++) {
+        for (size_t j = 0; j < S; j++) {
+            const bool d = (types[j] >> i) & 1;
+            const bool flip = (flag & PBG_F_OUTGROUP) && ((types[j] >> outidx) & 1);
+            out += d != flip ? '1' : '0';
+        }
+        out += "\n";
     }
     out += "\n";
 }

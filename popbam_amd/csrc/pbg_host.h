@@ -29,5 +29,10 @@ void format_window(std::string &out, const pbg_cmd &cmd, int n_samples, int n_po
 // print_popbam_snp (pop_snp.cpp:224-241) for one position's consensus words
 void format_snp_site(std::string &out, const pbg_cmd &cmd, int n_samples, int32_t pos, unsigned char refc,
                      const uint64_t *cb);
+void format_sweep_site(std::string &out, const pbg_cmd &cmd, int n_pops, const uint64_t *pop_mask, uint32_t flag,
+                       int32_t pos, uint64_t types);
+void format_ms_header(std::string &out, int n_samples, int n_pops, const int32_t *pop_n, long n_windows);
+void format_ms_window(std::string &out, int n_samples, uint32_t flag, int outidx, int32_t wbeg, int32_t wend,
+                      const std::vector<int32_t> &pos, const std::vector<uint64_t> &types);
 
 }  // namespace pbg

@@ -114,6 +114,15 @@ SCENARIOS = {
                               ["snp", "REGION=chr1:4001-4800"], ["nucdiv", "-w", "1", "-m", "0", "-q", "0"],
                               ["sfs", "-w", "1", "-m", "0", "-q", "0"], ["snp", "-m", "0", "-q", "0", "REGION=chr1:6500-8500"]],
                         gap=[(7000, 7600)]),
+    # G13: snp output formats -o 1 (SweepFinder) / -o 2 (ms), windows, outgroup flip, 3 populations
+    "g13_snpformats": dict(seed=1313, L=12000, samples=_samples(12, ["p1", "p2", "p3"]), step=10, mu=0.03,
+                           cmds=[["snp", "-o", "1"], ["snp", "-o", "2"], ["snp", "-o", "1", "-w", "2"],
+                                 ["snp", "-o", "2", "-w", "2"], ["snp", "-o", "1", "-p", "s3"],
+                                 ["snp", "-o", "2", "-w", "3", "-p", "s3"], ["snp", "-o", "2", "REGION=chr1:2001-5000"],
+                                 ["snp", "-o", "1", "-w", "1", "REGION=chr1:2501-9000"]]),
+    # G14: one population (ms header without -I)
+    "g14_onepop": dict(seed=1414, L=6000, samples=_samples(6, ["solo"]), step=10, mu=0.03,
+                       cmds=[["snp", "-o", "2"], ["snp", "-o", "2", "-w", "1"], ["snp", "-o", "1"], ["nucdiv", "-w", "1"]]),
 }
 
 
