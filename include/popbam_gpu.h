@@ -106,6 +106,7 @@ typedef struct { int32_t beg, end; } pbg_window;   /* row index range [beg, end)
 #define PBG_S_HAP_K    0x080   /* haplo -o 0            (pop_haplo.cpp:208-254)       */
 #define PBG_S_HAP_EHHS 0x100   /* haplo -o 1            (pop_haplo.cpp:256-323)       */
 #define PBG_S_HAP_DXY  0x200   /* haplo -o 2            (pop_haplo.cpp:325-363)       */
+#define PBG_S_TREE     0x400   /* tree diff_matrix      (pop_tree.cpp:472-494)        */
 
 typedef struct {
     uint32_t stats;        /* PBG_S_* mask; at most one of ZNS / OMEGA / WALL (they share
@@ -134,6 +135,9 @@ typedef struct {
     double   *hap_val;     /* [n_win*n_pops]            haplo Kdiv (1-hdiv) / EHHS / pi   */
     double   *hap_dxy;     /* [n_win*n_pops*(n_pops-1)] haplo -o 2 dxy                    */
     int32_t  *hap_min;     /* [n_win*n_pops*(n_pops-1)] haplo -o 2 min (u16)              */
+    int32_t  *tree_diff;   /* [n_win*(n+1)*(n+1)]       tree diff_matrix (u16 values): taxon 0
+                              = the reference (differences = derived count), taxon i+1 =
+                              sample i; the neighbour-joining tree is built on the host      */
 } pbg_window_out;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -158,8 +162,8 @@ int pbg_window_stats(pbg_ctx *ctx, const void *rows, uint32_t n_rows, const pbg_
                      void *stream);
 
 /* ---- one subcommand end to end ------------------------------------------------------ */
-enum { PBG_CMD_SNP = 0, PBG_CMD_HAPLO = 1, PBG_CMD_DIVERGE = 2, PBG_CMD_NUCDIV = 4,
-       PBG_CMD_LD = 5, PBG_CMD_SFS = 6 };   /* popbam_func_t values (popbam.h:208)       */
+enum { PBG_CMD_SNP = 0, PBG_CMD_HAPLO = 1, PBG_CMD_DIVERGE = 2, PBG_CMD_TREE = 3,
+       PBG_CMD_NUCDIV = 4, PBG_CMD_LD = 5, PBG_CMD_SFS = 6 };   /* popbam_func_t (popbam.h:208) */
 
 typedef struct {
     int32_t  cmd;          /* PBG_CMD_*                                                   */
@@ -168,13 +172,15 @@ typedef struct {
     int32_t  min_snps;     /* ld -n                                                       */
     int32_t  min_freq;     /* ld 1 / 2 (-e)                                               */
     int32_t  outidx;       /* -p sample index                                             */
-    int32_t  jc;           /* diverge -d jc                                               */
+    int32_t  jc;           /* diverge / tree -d jc                                        */
     int32_t  windowed;     /* -w given                                                    */
     int64_t  win_size;     /* bases                                                       */
     int32_t  beg, end;     /* parsed region [beg, end) in contig coordinates              */
     const char *chr_name;
     const char *const *sample_names;
     const char *const *pop_names;
+    const char *refid;     /* tree: taxon name of the reference (get_refid, pop_utils.cpp:463-498:
+                              the header's first AS: tag value)                              */
 } pbg_cmd;
 
 /* Runs `popbam <cmd>` over a HOST pileup batch that covers contig positions

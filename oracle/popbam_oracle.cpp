@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <list>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -850,6 +851,161 @@ void add_site(Window &W, const orc_params *p, uint32_t pos, uint64_t ty, uint8_t
     W.num_sites++;
 }
 
+// ---- tree: calc_diff_matrix pop_tree.cpp:472-494, calc_dist_matrix 496-515, make_nj 208-252,
+//      join_tree 254-429, print_tree 439-470.  Pointer rings as tree_init builds them.
+struct TNode {
+    TNode *next = nullptr, *back = nullptr;
+    int index = 0;
+    bool tip = false;
+    double v = 0.0;
+};
+
+void t_print(Out &o, const TNode *p, const TNode *start, const char *refid, const char *const *smpl) {
+    if (p->tip) {
+        o.str(p->index == 1 ? refid : smpl[p->index - 2]);
+    } else {
+        o.str("(");
+        t_print(o, p->next->back, start, refid, smpl);
+        o.str(",");
+        t_print(o, p->next->next->back, start, refid, smpl);
+        if (p == start) {
+            o.str(",");
+            t_print(o, p->back, start, refid, smpl);
+        }
+        o.str(")");
+    }
+    if (p == start) o.str(";\n");
+    else if (p->v < 0) o.str(":0.00000");
+    else { o.str(":"); o.f(p->v); }
+}
+
+void do_tree(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
+    const int n = p->n_samples, ntaxa = n + 1;
+    if (W.num_sites < c->min_sites || W.segsites < 1) {
+        head(o, c, W);
+        o.str("\tNA\n");
+        return;
+    }
+    std::vector<std::vector<uint16_t>> diff(ntaxa, std::vector<uint16_t>(ntaxa, 0));
+    int words = (W.segsites - 1) / 64;
+    for (int i = 0; i < n; i++) {
+        for (int k = 0; k <= words; k++) diff[i + 1][0] += popcnt64(W.seq[i][k]);
+        diff[0][i + 1] = diff[i + 1][0];
+    }
+    for (int i = 0; i < n - 1; i++)
+        for (int j = i + 1; j < n; j++) {
+            for (int k = 0; k <= words; k++) diff[j + 1][i + 1] += popcnt64(W.seq[i][k] ^ W.seq[j][k]);
+            diff[i + 1][j + 1] = diff[j + 1][i + 1];
+        }
+    std::vector<std::vector<double>> x(ntaxa, std::vector<double>(ntaxa, 0.0));
+    for (int i = 0; i < ntaxa - 1; i++)
+        for (int j = i + 1; j < ntaxa; j++) {
+            x[i][j] = (double)diff[i][j] / W.num_sites;
+            x[j][i] = x[i][j];
+            if (c->jc) {
+                x[i][j] = -0.75 * std::log(1.0 - (4.0 * x[i][j] / 3.0));
+                x[j][i] = x[i][j];
+            }
+        }
+    // tree_init + make_nj's trim of the last ring + setup_tree
+    const int nnodes = 2 * ntaxa - 1;
+    std::vector<std::unique_ptr<TNode>> pool;
+    std::vector<TNode *> nodep(nnodes);
+    auto mk = [&]() { pool.emplace_back(new TNode()); return pool.back().get(); };
+    for (int i = 0; i < ntaxa; i++) nodep[i] = mk();
+    for (int i = ntaxa; i < nnodes; i++) {
+        TNode *q = nullptr, *pp = nullptr;
+        for (int j = 1; j <= 3; j++) { pp = mk(); pp->next = q; q = pp; }
+        pp->next->next->next = pp;
+        nodep[i] = pp;
+    }
+    nodep[nnodes - 1]->next = nodep[nnodes - 1];
+    for (int i = 1; i <= nnodes; i++) {
+        TNode *h = nodep[i - 1];
+        h->back = nullptr; h->tip = i <= ntaxa; h->index = i; h->v = 0.0;
+        if (i > ntaxa)
+            for (TNode *q = h->next; q != h; q = q->next) { q->back = nullptr; q->tip = false; q->index = i; }
+    }
+    auto hookup = [](TNode *a, TNode *b) { a->back = b; b->back = a; };
+    std::vector<TNode *> cluster(nodep.begin(), nodep.begin() + ntaxa);
+    std::vector<int> enterorder(ntaxa);
+    for (int i = 0; i < ntaxa; i++) enterorder[i] = i + 1;
+    // join_tree
+    for (int i = 0; i < ntaxa - 1; i++)
+        for (int j = i + 1; j < ntaxa; j++) {
+            double da = (x[i][j] + x[j][i]) / 2.0;
+            x[i][j] = da; x[j][i] = da;
+        }
+    double fotu2 = ntaxa - 2.0, total = 0, tmin, dio, djo, bi, bj, bk, dmin;
+    int nextnode = ntaxa + 1, mini = 0, minj = 0;
+    std::vector<double> av(ntaxa, 0.0), R(ntaxa);
+    for (int nc = 1; nc <= ntaxa - 3; nc++) {
+        for (int j = 2; j <= ntaxa; j++)
+            for (int i = 0; i <= j - 2; i++) x[j - 1][i] = x[i][j - 1];
+        tmin = DBL_MAX;
+        for (int i = 0; i < ntaxa; i++) R[i] = 0.0;
+        for (int ja = 2; ja <= ntaxa; ja++) {
+            int jj = enterorder[ja - 1];
+            if (cluster[jj - 1] != nullptr)
+                for (int ia = 0; ia <= ja - 2; ia++) {
+                    int ii = enterorder[ia];
+                    if (cluster[ii - 1] != nullptr) { R[ii - 1] += x[ii - 1][jj - 1]; R[jj - 1] += x[ii - 1][jj - 1]; }
+                }
+        }
+        for (int ja = 2; ja <= ntaxa; ja++) {
+            int jj = enterorder[ja - 1];
+            if (cluster[jj - 1] != nullptr)
+                for (int ia = 0; ia <= ja - 2; ia++) {
+                    int ii = enterorder[ia];
+                    if (cluster[ii - 1] != nullptr) total = fotu2 * x[ii - 1][jj - 1] - R[ii - 1] - R[jj - 1];
+                    if (total < tmin) { tmin = total; mini = ii; minj = jj; }
+                }
+        }
+        dio = 0.0; djo = 0.0;
+        for (int i = 0; i < ntaxa; i++) { dio += x[i][mini - 1]; djo += x[i][minj - 1]; }
+        dmin = x[mini - 1][minj - 1];
+        dio = (dio - dmin) / fotu2;
+        djo = (djo - dmin) / fotu2;
+        bi = (dmin + dio - djo) * 0.5;
+        bj = dmin - bi;
+        bi -= av[mini - 1];
+        bj -= av[minj - 1];
+        hookup(nodep[nextnode - 1]->next, cluster[mini - 1]);
+        hookup(nodep[nextnode - 1]->next->next, cluster[minj - 1]);
+        cluster[mini - 1]->v = bi; cluster[minj - 1]->v = bj;
+        cluster[mini - 1]->back->v = bi; cluster[minj - 1]->back->v = bj;
+        cluster[mini - 1] = nodep[nextnode - 1];
+        cluster[minj - 1] = nullptr;
+        nextnode++;
+        av[mini - 1] = dmin * 0.5;
+        fotu2 -= 1.0;
+        for (int j = 0; j < ntaxa; j++)
+            if (cluster[j] != nullptr) {
+                double da = (x[mini - 1][j] + x[minj - 1][j]) * 0.5;
+                if (mini - j - 1 < 0) x[mini - 1][j] = da;
+                if (mini - j - 1 > 0) x[j][mini - 1] = da;
+            }
+        for (int j = 0; j < ntaxa; j++) { x[minj - 1][j] = 0.0; x[j][minj - 1] = 0.0; }
+    }
+    int el[3] = {0, 0, 0}, nude = 1;
+    for (int i = 1; i <= ntaxa; i++)
+        if (cluster[i - 1] != nullptr) { el[nude - 1] = i; nude++; }
+    bi = (x[el[0] - 1][el[1] - 1] + x[el[0] - 1][el[2] - 1] - x[el[1] - 1][el[2] - 1]) * 0.5;
+    bj = x[el[0] - 1][el[1] - 1] - bi;
+    bk = x[el[0] - 1][el[2] - 1] - bi;
+    bi -= av[el[0] - 1]; bj -= av[el[1] - 1]; bk -= av[el[2] - 1];
+    hookup(nodep[nextnode - 1], cluster[el[0] - 1]);
+    hookup(nodep[nextnode - 1]->next, cluster[el[1] - 1]);
+    hookup(nodep[nextnode - 1]->next->next, cluster[el[2] - 1]);
+    cluster[el[0] - 1]->v = bi; cluster[el[1] - 1]->v = bj; cluster[el[2] - 1]->v = bk;
+    cluster[el[0] - 1]->back->v = bi; cluster[el[1] - 1]->back->v = bj; cluster[el[2] - 1]->back->v = bk;
+    // make_nj: print from the node the reference taxon hangs on
+    TNode *start = nodep[0]->back;
+    head(o, c, W);
+    o.str("\t");
+    t_print(o, start, start, c->refid ? c->refid : "", c->sample_names);
+}
+
 void init_window(Window &W, const orc_params *p, int b, int e) {
     int n = p->n_samples;
     W = Window();
@@ -865,6 +1021,7 @@ void emit(Out &o, const orc_params *p, const orc_cmd *c, const Window &W, const 
         case ORC_LD: do_ld(o, p, c, W); break;
         case ORC_DIVERGE: do_diverge(o, p, c, W); break;
         case ORC_HAPLO: do_haplo(o, p, c, W); break;
+        case ORC_TREE: do_tree(o, p, c, W); break;
         case ORC_SNP:
             if (c->output == 1) do_sweep(o, p, c, W);
             else if (c->output == 2) do_ms(o, p, c, W);

@@ -21,6 +21,7 @@ PBG_OK, PBG_E_ARG, PBG_E_HIP, PBG_E_NOMEM, PBG_E_RANGE, PBG_E_NODEV = 0, -1, -2,
 
 PBG_S_NUCDIV, PBG_S_SFS, PBG_S_ZNS, PBG_S_OMEGA, PBG_S_WALL = 0x1, 0x2, 0x4, 0x8, 0x10
 PBG_S_DIV_IND, PBG_S_DIV_POP, PBG_S_HAP_K, PBG_S_HAP_EHHS, PBG_S_HAP_DXY = 0x20, 0x40, 0x80, 0x100, 0x200
+PBG_S_TREE = 0x400
 
 # every symbol include/popbam_gpu.h declares
 EXPORTS = ["pbg_create", "pbg_destroy", "pbg_last_error", "pbg_row_bytes", "pbg_device_count",
@@ -51,14 +52,15 @@ class PbgStatOpts(C.Structure):
 class PbgWindowOut(C.Structure):
     _fields_ = [(nm, C.c_void_p) for nm in
                 ("num_sites", "segsites", "pi", "dxy", "td", "fwh", "ld_snps", "ld_val", "ld_q", "div_ind",
-                 "div_fixed", "div_seg", "div_pop", "nhaps", "hap_val", "hap_dxy", "hap_min")]
+                 "div_fixed", "div_seg", "div_pop", "nhaps", "hap_val", "hap_dxy", "hap_min", "tree_diff")]
 
 
 class PbgCmd(C.Structure):
     _fields_ = [("cmd", C.c_int32), ("output", C.c_int32), ("min_sites", C.c_int32), ("min_snps", C.c_int32),
                 ("min_freq", C.c_int32), ("outidx", C.c_int32), ("jc", C.c_int32), ("windowed", C.c_int32),
                 ("win_size", C.c_int64), ("beg", C.c_int32), ("end", C.c_int32), ("chr_name", C.c_char_p),
-                ("sample_names", C.POINTER(C.c_char_p)), ("pop_names", C.POINTER(C.c_char_p))]
+                ("sample_names", C.POINTER(C.c_char_p)), ("pop_names", C.POINTER(C.c_char_p)),
+                ("refid", C.c_char_p)]
 
 
 _lib = None

@@ -1,15 +1,15 @@
 """`popbam <cmd> [options] <in.bam> <region>` on the GPU: the drop-in command line.
 
 Mirrors POPBAM's main (popbam.cpp:53-77) and main_<cmd> (e.g. pop_nucdiv.cpp:10-134) for the
-subcommands on the hot path -- snp, nucdiv, sfs, ld, diverge, haplo:
+subcommands snp, nucdiv, sfs, ld, diverge, haplo and tree:
   parseCommandLine (GetOpt_pp quirks, options.parse_args)
   -> checkBAM (popbam.cpp:95-143: BAM, optional -h header text, .bai, FASTA)
   -> bam_smpl_add (options.parse_header) -> bam_parse_region (options.parse_region)
   -> faidx_fetch_seq of the contig -> one pileup of the region (libpopbam_feed.so)
   -> pbg_run (libpopbam_gpu.so: consensus call, the reference's window loop, print_<cmd>).
 stdout is the reference's TSV byte for byte; errors are reported like fatal_error
-(pop_utils.cpp:510-519) with exit status 1.  `tree` (neighbour joining) is not on the GPU
-path and is rejected.
+(pop_utils.cpp:510-519) with exit status 1.  `tree` (main_tree, pop_tree.cpp:10-136) takes its
+per-window diff_matrix from the GPU and joins the (n+1)-taxon tree on the host.
 """
 from __future__ import annotations
 
@@ -18,7 +18,7 @@ import sys
 
 from . import options as opt
 
-COMMANDS = ("snp", "haplo", "diverge", "nucdiv", "ld", "sfs")
+COMMANDS = ("snp", "haplo", "diverge", "tree", "nucdiv", "ld", "sfs")
 
 USAGE = """
 Program: popbam (MI355X hot path: consensus call + window statistics on the GPU)
@@ -28,6 +28,7 @@ Usage:   popbam <command> [options] <in.bam> <region>
 Command: snp         call SNPs
          haplo       haplotype-based statistics
          diverge     divergence from the reference
+         tree        neighbour-joining tree per window (pdist or jc)
          nucdiv      nucleotide diversity (pi, dxy)
          ld          linkage disequilibrium (ZnS, omega_max, Wall's B/Q)
          sfs         site frequency spectrum (Tajima's D, Fay-Wu H)
@@ -60,6 +61,7 @@ def run(cmd: str, argv: list[str], device: int = 0) -> str:
         if not o.reffile or not os.path.exists(o.reffile):
             raise opt.PopbamError(f"Failed to load index for fastA reference file: {o.reffile}")
         sm = opt.parse_header(header, o.bamfile)
+        refid = opt.get_refid(header) if cmd == "tree" else ""
         refs = bam.refs
         names, lengths = [r[0] for r in refs], [r[1] for r in refs]
         tid, beg, end = opt.parse_region(o.region, names, lengths)
@@ -73,7 +75,7 @@ def run(cmd: str, argv: list[str], device: int = 0) -> str:
             if e.code == feed.PBF_E_RG:
                 raise opt.PopbamError("Problem assigning read group") from e
             raise opt.PopbamError(f"Failed to retrieve region {o.region}: {e}") from e
-        return engine.run_command(o, sm, names[tid], beg, end, batch, pos0=beg, device=device)
+        return engine.run_command(o, sm, names[tid], beg, end, batch, pos0=beg, device=device, refid=refid)
     finally:
         bam.close()
 
@@ -85,10 +87,7 @@ def main(argv: list[str] | None = None) -> int:
         return 1
     cmd = argv[0]
     if cmd not in COMMANDS:
-        if cmd == "tree":
-            sys.stderr.write("Error: the tree command is not part of the GPU hot path\n")
-        else:
-            sys.stderr.write(f"Error: unrecognized command: {cmd}\n")
+        sys.stderr.write(f"Error: unrecognized command: {cmd}\n")
         return 1
     try:
         text = run(cmd, argv[1:], device=int(os.environ.get("POPBAM_DEVICE", "0")))

@@ -522,6 +522,11 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
             case PBG_CMD_HAPLO:
                 stats = cmd->output == 1 ? PBG_S_HAP_EHHS : cmd->output == 2 ? PBG_S_HAP_DXY : PBG_S_HAP_K;
                 break;
+            case PBG_CMD_TREE:
+                // join_tree's last cycle needs three clusters (ntaxa = n + 1 >= 3)
+                if (n < 2) return fail(c, PBG_E_ARG, "tree needs at least two samples");
+                stats = PBG_S_TREE;
+                break;
             default: return fail(c, PBG_E_ARG, "unsupported subcommand");
         }
         const uint32_t nw = (uint32_t)win.size();
@@ -535,7 +540,8 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         }
         const int npairs = std::max(1, np * (np - 1));
         const size_t szw = nw, szp = (size_t)nw * np, szq = (size_t)nw * npairs, szn = (size_t)nw * n;
-        DevBuf o_ns, o_seg, o_d1, o_d2, o_d3, o_i1, o_i2, o_i3;
+        const size_t szt = stats == PBG_S_TREE ? (size_t)nw * (n + 1) * (n + 1) : 1;
+        DevBuf o_ns, o_seg, o_d1, o_d2, o_d3, o_i1, o_i2, o_i3, o_td;
         HIPCHK(c, d_win.alloc(nw * sizeof(pbg_window)));
         HIPCHK(c, hipMemcpy(d_win.p, rw.data(), nw * sizeof(pbg_window), hipMemcpyHostToDevice));
         HIPCHK(c, o_ns.alloc(szw * 4));
@@ -546,6 +552,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         HIPCHK(c, o_i1.alloc(szp * 4));
         HIPCHK(c, o_i2.alloc(szp * 4));
         HIPCHK(c, o_i3.alloc(szq * 4));
+        HIPCHK(c, o_td.alloc(szt * 4));
         pbg_window_out O{};
         O.num_sites = (int32_t *)o_ns.p;
         O.segsites = (int32_t *)o_seg.p;
@@ -561,6 +568,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
             case PBG_S_HAP_K: O.nhaps = i1; O.hap_val = d1; break;
             case PBG_S_HAP_EHHS: O.hap_val = d1; break;
             case PBG_S_HAP_DXY: O.hap_val = d3; O.hap_dxy = d1; O.hap_min = i3; break;
+            case PBG_S_TREE: O.tree_diff = (int32_t *)o_td.p; break;
         }
         pbg_stat_opts so{stats, cmd->min_freq, cmd->outidx, cmd->jc};
         // an all-empty batch still needs one addressable row for the kernel's pointer
@@ -574,13 +582,14 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         int rc = pbg_window_stats(c, rows_p, dsites, (const pbg_window *)d_win.p, nw, &so, &O, s);
         if (rc) return rc;
         HIPCHK(c, hipDeviceSynchronize());
-        std::vector<int32_t> h_ns(szw), h_seg(szw), h_i1(szp), h_i2(szp), h_i3(szq);
+        std::vector<int32_t> h_ns(szw), h_seg(szw), h_i1(szp), h_i2(szp), h_i3(szq), h_td(szt);
         std::vector<double> h_d1(std::max(szq, std::max(szp, szn))), h_d2(std::max(szq, szp)), h_d3(szp);
         HIPCHK(c, hipMemcpy(h_ns.data(), o_ns.p, szw * 4, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_seg.data(), o_seg.p, szw * 4, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_i1.data(), o_i1.p, szp * 4, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_i2.data(), o_i2.p, szp * 4, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_i3.data(), o_i3.p, szq * 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(h_td.data(), o_td.p, szt * 4, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_d1.data(), o_d1.p, h_d1.size() * 8, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_d2.data(), o_d2.p, h_d2.size() * 8, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_d3.data(), o_d3.p, h_d3.size() * 8, hipMemcpyDeviceToHost));
@@ -611,6 +620,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
                 case PBG_S_HAP_DXY:
                     wh.hap_val = slice(h_d3, i * np, np); wh.hap_dxy = slice(h_d1, i * npairs, npairs);
                     wh.hap_min = slice(h_i3, i * npairs, npairs); break;
+                case PBG_S_TREE: wh.tree_diff = slice(h_td, i * (n + 1) * (n + 1), (size_t)(n + 1) * (n + 1)); break;
             }
             pbg::format_window(text, *cmd, n, np, c->dp.flag, wh);
         }
@@ -651,6 +661,7 @@ long pbg_format(const pbg_ctx *c, const pbg_cmd *cmd, const pbg_window_out *ho, 
         wh.hap_val = take(ho->hap_val, (size_t)i * np, np);
         wh.hap_dxy = take(ho->hap_dxy, (size_t)i * npairs, npairs);
         wh.hap_min = take(ho->hap_min, (size_t)i * npairs, npairs);
+        wh.tree_diff = take(ho->tree_diff, (size_t)i * (n + 1) * (n + 1), (size_t)(n + 1) * (n + 1));
         pbg::format_window(text, *cmd, n, np, c->dp.flag, wh);
     }
     if (needed) *needed = text.size() + 1;

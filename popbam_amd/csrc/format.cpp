@@ -3,6 +3,7 @@
 // The reference streams to std::cout with `std::fixed << std::setprecision(5)` (sticky),
 // which libstdc++ renders through printf's "%.5f"; "NA" cells are `"\t" << std::setw(7) <<
 // "NA"`, i.e. five spaces then NA.  Integers print in decimal.
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <string>
@@ -28,6 +29,209 @@ struct W {
 };
 
 std::string pn(const pbg_cmd &c, int i) { return c.pop_names[i]; }
+
+// ---- tree (pop_tree.cpp): distances, neighbour joining and the Newick printer.
+// The tree is O(ntaxa^3) scalar work on an (n+1)x(n+1) matrix per window, so it runs on the
+// host on the GPU's diff_matrix.  Nodes live in one array; a ring of three nodes is one
+// internal node as in tree_init (pop_tree.cpp:517-539), -1 is the null pointer.
+struct NjNode {
+    int next = -1, back = -1, index = 0;
+    bool tip = false;
+    double v = 0.0;
+};
+
+struct Nj {
+    int ntaxa;
+    std::vector<NjNode> nd;
+    std::vector<int> nodep;   // curtree.nodep
+
+    explicit Nj(int nt) : ntaxa(nt) {
+        const int nnodes = 2 * nt - 1;
+        nodep.resize(nnodes);
+        for (int i = 0; i < nnodes; ++i) {
+            const int h = (int)nd.size();
+            if (i < nt) {
+                nd.emplace_back();
+            } else {   // ring head -> a -> b -> head
+                nd.resize(nd.size() + 3);
+                nd[h].next = h + 1;
+                nd[h + 1].next = h + 2;
+                nd[h + 2].next = h;
+            }
+            nodep[i] = h;
+        }
+        nd[nodep[nnodes - 1]].next = nodep[nnodes - 1];   // make_nj: last ring cut to one node
+        for (int i = 1; i <= nnodes; ++i) {                // setup_tree pop_tree.cpp:541-566
+            NjNode &q = nd[nodep[i - 1]];
+            q.back = -1;
+            q.tip = i <= nt;
+            q.index = i;
+            q.v = 0.0;
+            if (i > nt)
+                for (int r = q.next; r != nodep[i - 1]; r = nd[r].next) {
+                    nd[r].back = -1;
+                    nd[r].tip = false;
+                    nd[r].index = i;
+                }
+        }
+    }
+    void hookup(int p, int q) {
+        nd[p].back = q;
+        nd[q].back = p;
+    }
+    void set_len(int c, double v) {
+        nd[c].v = v;
+        nd[nd[c].back].v = v;
+    }
+
+    // join_tree pop_tree.cpp:254-429, statement for statement (including `total` carried over
+    // from a skipped pair and across cycles, and the column sums over cleared rows)
+    void join(std::vector<double> x) {
+        const int nt = ntaxa;
+        auto X = [&](int i, int j) -> double & { return x[(size_t)i * nt + j]; };
+        std::vector<int> cluster(nt), eo(nt);
+        std::vector<double> av(nt, 0.0), R(nt);
+        for (int i = 0; i < nt; ++i) {
+            cluster[i] = nodep[i];
+            eo[i] = i + 1;
+        }
+        for (int i = 0; i < nt - 1; i++)
+            for (int j = i + 1; j < nt; j++) {
+                const double da = (X(i, j) + X(j, i)) / 2.0;
+                X(i, j) = da;
+                X(j, i) = da;
+            }
+        double fotu2 = nt - 2.0, total = 0, tmin, dio, djo, bi, bj, bk, dmin;
+        int nextnode = nt + 1, mini = 0, minj = 0;
+        for (int nc = 1; nc <= nt - 3; nc++) {
+            for (int j = 2; j <= nt; j++)
+                for (int i = 0; i <= j - 2; i++) X(j - 1, i) = X(i, j - 1);
+            tmin = DBL_MAX;
+            for (int i = 0; i < nt; i++) R[i] = 0.0;
+            for (int ja = 2; ja <= nt; ja++) {
+                const int jj = eo[ja - 1];
+                if (cluster[jj - 1] < 0) continue;
+                for (int ia = 0; ia <= ja - 2; ia++) {
+                    const int ii = eo[ia];
+                    if (cluster[ii - 1] >= 0) {
+                        R[ii - 1] += X(ii - 1, jj - 1);
+                        R[jj - 1] += X(ii - 1, jj - 1);
+                    }
+                }
+            }
+            for (int ja = 2; ja <= nt; ja++) {
+                const int jj = eo[ja - 1];
+                if (cluster[jj - 1] < 0) continue;
+                for (int ia = 0; ia <= ja - 2; ia++) {
+                    const int ii = eo[ia];
+                    if (cluster[ii - 1] >= 0) total = fotu2 * X(ii - 1, jj - 1) - R[ii - 1] - R[jj - 1];
+                    if (total < tmin) {
+                        tmin = total;
+                        mini = ii;
+                        minj = jj;
+                    }
+                }
+            }
+            dio = 0.0;
+            djo = 0.0;
+            for (int i = 0; i < nt; i++) {
+                dio += X(i, mini - 1);
+                djo += X(i, minj - 1);
+            }
+            dmin = X(mini - 1, minj - 1);
+            dio = (dio - dmin) / fotu2;
+            djo = (djo - dmin) / fotu2;
+            bi = (dmin + dio - djo) * 0.5;
+            bj = dmin - bi;
+            bi -= av[mini - 1];
+            bj -= av[minj - 1];
+            const int h = nodep[nextnode - 1];
+            hookup(nd[h].next, cluster[mini - 1]);
+            hookup(nd[nd[h].next].next, cluster[minj - 1]);
+            set_len(cluster[mini - 1], bi);
+            set_len(cluster[minj - 1], bj);
+            cluster[mini - 1] = h;
+            cluster[minj - 1] = -1;
+            nextnode++;
+            av[mini - 1] = dmin * 0.5;
+            fotu2 -= 1.0;
+            for (int j = 0; j < nt; j++)
+                if (cluster[j] >= 0) {
+                    const double da = (X(mini - 1, j) + X(minj - 1, j)) * 0.5;
+                    if (mini - j - 1 < 0) X(mini - 1, j) = da;
+                    if (mini - j - 1 > 0) X(j, mini - 1) = da;
+                }
+            for (int j = 0; j < nt; j++) {
+                X(minj - 1, j) = 0.0;
+                X(j, minj - 1) = 0.0;
+            }
+        }
+        int el[3] = {0, 0, 0}, nude = 1;
+        for (int i = 1; i <= nt && nude <= 3; i++)
+            if (cluster[i - 1] >= 0) el[nude++ - 1] = i;
+        bi = (X(el[0] - 1, el[1] - 1) + X(el[0] - 1, el[2] - 1) - X(el[1] - 1, el[2] - 1)) * 0.5;
+        bj = X(el[0] - 1, el[1] - 1) - bi;
+        bk = X(el[0] - 1, el[2] - 1) - bi;
+        bi -= av[el[0] - 1];
+        bj -= av[el[1] - 1];
+        bk -= av[el[2] - 1];
+        const int h = nodep[nextnode - 1];
+        hookup(h, cluster[el[0] - 1]);
+        hookup(nd[h].next, cluster[el[1] - 1]);
+        hookup(nd[nd[h].next].next, cluster[el[2] - 1]);
+        set_len(cluster[el[0] - 1], bi);
+        set_len(cluster[el[1] - 1], bj);
+        set_len(cluster[el[2] - 1], bk);
+    }
+
+    // print_tree pop_tree.cpp:439-470
+    void print(W &o, int p, int start, const char *refid, const char *const *names) const {
+        const NjNode &q = nd[p];
+        if (q.tip) {
+            o.t(q.index == 1 ? refid : names[q.index - 2]);
+        } else {
+            o.t("(");
+            print(o, nd[q.next].back, start, refid, names);
+            o.t(",");
+            print(o, nd[nd[q.next].next].back, start, refid, names);
+            if (p == start) {
+                o.t(",");
+                print(o, q.back, start, refid, names);
+            }
+            o.t(")");
+        }
+        if (p == start) {
+            o.t(";");
+        } else if (q.v < 0) {
+            o.t(":0.00000");
+        } else {
+            o.t(":");
+            o.f(q.v);
+        }
+    }
+};
+
+// make_nj pop_tree.cpp:208-252 after calc_dist_matrix 496-515 (the caller prints the row head)
+void format_nj(W &o, const pbg_cmd &c, int n, const WindowHost &w) {
+    if (w.num_sites < c.min_sites || w.segsites < 1) {
+        o.t("\tNA");
+        return;
+    }
+    const int nt = n + 1;
+    std::vector<double> dist((size_t)nt * nt, 0.0);
+    for (int i = 0; i < nt - 1; i++)
+        for (int j = i + 1; j < nt; j++) {
+            double d = (double)w.tree_diff[(size_t)i * nt + j] / w.num_sites;
+            if (c.jc) d = -0.75 * std::log(1.0 - (4.0 * d / 3.0));
+            dist[(size_t)i * nt + j] = d;
+            dist[(size_t)j * nt + i] = d;
+        }
+    Nj t(nt);
+    t.join(dist);
+    const int start = t.nd[t.nodep[0]].back;
+    o.t("\t");
+    t.print(o, start, start, c.refid ? c.refid : "", c.sample_names);
+}
 
 }  // namespace
 
@@ -137,6 +341,9 @@ void format_window(std::string &out, const pbg_cmd &c, int n, int np, uint32_t f
                         if (ok) o.i(w.hap_min[k]); else o.na();
                     }
             }
+            break;
+        case PBG_CMD_TREE:
+            format_nj(o, c, n, w);
             break;
         default:
             break;

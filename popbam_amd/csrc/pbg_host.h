@@ -19,7 +19,7 @@ struct WindowHost {
     int32_t beg = 0, end = 0;       // contig coordinates [beg, end)
     int32_t num_sites = 0, segsites = 0;
     std::vector<double> pi, dxy, td, fwh, ld_val, ld_q, div_ind, div_pop, hap_val, hap_dxy;
-    std::vector<int32_t> ld_snps, div_fixed, div_seg, nhaps, hap_min;
+    std::vector<int32_t> ld_snps, div_fixed, div_seg, nhaps, hap_min, tree_diff;
 };
 
 // print_nucdiv / print_sfs / print_ld / print_diverge / print_haplo (TSV, byte-identical)

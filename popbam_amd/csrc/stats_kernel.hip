@@ -122,7 +122,8 @@ __global__ __launch_bounds__(kBlockThreads) void window_stats_kernel(DevParams P
 
     // types of the j-th segregating site: seg[j] (== types[hap.idx[j]] in the reference)
     const int nwords = S > 0 ? (S + 63) / 64 : 1;
-    const bool need_planes = (A.stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY)) != 0;
+    const bool need_planes = (A.stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY |
+                                         PBG_S_TREE)) != 0;
     uint64_t *plane = nullptr;
     if (need_planes) {
         plane = (n * nwords <= kPlaneCap) ? s_plane : (A.ws + A.ws_off[w] + ws_plane_off(len));
@@ -264,6 +265,25 @@ __global__ __launch_bounds__(kBlockThreads) void window_stats_kernel(DevParams P
         double pd = (double)(d & 0xFFFF) / num_sites;
         double v = A.jc ? -0.75 * log(1.0 - pd * (4.0 / 3.0)) : pd;
         if (O.div_ind) O.div_ind[(size_t)w * n + tid] = x86nan(v);
+    }
+    // ---- tree: treeData's diff_matrix (calc_diff_matrix, pop_tree.cpp:472-494), u16 values;
+    //      taxon 0 is the reference (row = the sample's derived count), taxon i+1 sample i
+    if ((A.stats & PBG_S_TREE) && O.tree_diff) {
+        const int nt = n + 1;
+        int32_t *td = O.tree_diff + (size_t)w * nt * nt;
+        for (int pr = tid; pr < nt * nt; pr += kBlockThreads) {
+            const int a = pr / nt, b = pr - a * nt;
+            int32_t v = 0;
+            if (a != b && (a == 0 || b == 0)) {
+                const int sm = a + b - 1;
+                uint32_t d = 0;
+                for (int k = 0; k < nwords; ++k) d += pc(plane[sm * nwords + k]);
+                v = (int32_t)(d & 0xFFFF);
+            } else if (a != b) {
+                v = s_diff[(a - 1) * n + (b - 1)];
+            }
+            td[pr] = v;
+        }
     }
     // ---- diverge -o 1 (lane per population)
     if ((A.stats & PBG_S_DIV_POP) && tid >= 64 && tid < 64 + np) {

@@ -31,7 +31,8 @@ def make_params(o: opt.Options, sm: opt.SampleModel) -> _lib.PbgParams:
 
 
 class _Cmd:
-    def __init__(self, o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, end: int):
+    def __init__(self, o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, end: int,
+                 refid: str = ""):
         c = _lib.PbgCmd()
         c.cmd = opt.CMD_IDS[o.cmd]
         c.output, c.min_sites, c.min_snps, c.min_freq = o.output, o.min_sites, o.min_snps, o.min_freq
@@ -51,11 +52,13 @@ class _Cmd:
         c.chr_name = self._chr
         c.sample_names = C.cast(self._sn, C.POINTER(C.c_char_p))
         c.pop_names = C.cast(self._pn, C.POINTER(C.c_char_p))
+        self._refid = refid.encode()
+        c.refid = self._refid
         self.c = c
 
 
 def run_command(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, end: int, batch: dict,
-                pos0: int = 0, device: int = 0, ctx: _lib.Context | None = None) -> str:
+                pos0: int = 0, device: int = 0, ctx: _lib.Context | None = None, refid: str = "") -> str:
     """batch: {'ref': u8[n_sites], 'depth': u16[n_sites, n], 'reads': u32[...]} (host)."""
     own = ctx is None
     if own:
@@ -67,7 +70,7 @@ def run_command(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, en
         if rd.size == 0:
             rd = np.zeros(1, np.uint32)
         pl = _lib.PbgPileup(len(ref), pos0, ref.ctypes.data, dep.ctypes.data, None, rd.ctypes.data)
-        cmd = _Cmd(o, sm, chr_name, beg, end)
+        cmd = _Cmd(o, sm, chr_name, beg, end, refid)
         need = C.c_size_t(0)
         cap = 1 << 20
         while True:
@@ -84,7 +87,7 @@ def run_command(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, en
 
 
 def run_command_sharded(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, end: int, batch: dict,
-                        pos0: int = 0, device: int = 0, group=None) -> str | None:
+                        pos0: int = 0, device: int = 0, group=None, refid: str = "") -> str | None:
     """run_command over this rank's block of windows (popbam_amd.shard), on this rank's GPU,
     with the TSV gathered to rank 0.  Each rank uploads only the positions its windows read."""
     from . import shard
@@ -94,6 +97,6 @@ def run_command_sharded(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg:
         lo, hi = shard.positions_needed(b, e, o.win_size, windowed)
         hi = max(hi, lo + 1)
         sub = shard.slice_batch(batch, pos0, lo, hi)
-        return run_command(o, sm, chr_name, b, e, sub, pos0=sub["pos0"], device=device)
+        return run_command(o, sm, chr_name, b, e, sub, pos0=sub["pos0"], device=device, refid=refid)
 
     return shard.run_sharded(block, beg, end, o.win_size, windowed, group)

@@ -75,9 +75,13 @@ _VALUE_OPTS = {
               ("a", "c"), ("b", "c"), ("k", "i"), ("w", "u")],
     "snp": [("f", "s"), ("h", "s"), ("m", "i"), ("x", "i"), ("q", "i"), ("s", "i"), ("a", "c"),
             ("b", "c"), ("o", "i"), ("z", "L"), ("p", "s"), ("w", "u")],
+    # treeData::parseCommandLine pop_tree.cpp:590-612
+    "tree": [("f", "s"), ("h", "s"), ("m", "i"), ("x", "i"), ("q", "i"), ("s", "i"), ("a", "c"),
+             ("b", "c"), ("k", "i"), ("w", "u"), ("d", "s")],
 }
 _PRESENT = {
     "nucdiv": "whpin", "sfs": "whpi", "ld": "whie", "diverge": "whpnti", "haplo": "whi", "snp": "whvizp",
+    "tree": "whi",
 }
 _ATTR = {"f": "reffile", "h": "headfile", "m": "min_depth", "x": "max_depth", "q": "min_rmsQ",
          "s": "min_snpQ", "a": "min_mapQ", "b": "min_baseQ", "k": "min_sites", "w": "win_size",
@@ -185,7 +189,7 @@ def parse_args(cmd: str, argv: list[str]) -> Options:
         o.flag |= BAM_VARIANT
     if cmd == "snp" and "z" in present:
         o.flag |= BAM_HETEROZYGOTE
-    if cmd == "diverge" and o.dist not in ("pdist", "jc"):
+    if cmd in ("diverge", "tree") and o.dist not in ("pdist", "jc"):
         raise PopbamError(f"{o.dist} is not a valid distance option")
     if cmd in ("ld", "haplo", "snp") and not 0 <= o.output <= 2:
         raise PopbamError("Not a valid output option")
@@ -234,6 +238,20 @@ def parse_region(region: str, names: list[str], lengths: list[int]):
     if beg > end:
         raise PopbamError(f"Bad genome coordinates: {region}")
     return tid, beg, end
+
+
+def get_refid(text: str) -> str:
+    """get_refid (pop_utils.cpp:463-498): the value of the header's first "AS:" tag, up to a
+    tab or newline (the tree's name for the reference taxon)."""
+    v = text.find("AS:")
+    if v < 0:
+        raise PopbamError("Unable to parse reference sequence name\n"
+                          "Be sure the AS tag is defined in the sequence dictionary")
+    u = v + 3
+    w = u
+    while w < len(text) and text[w] not in "\t\n":
+        w += 1
+    return text[u:w][:199]
 
 
 def _atoi(s):

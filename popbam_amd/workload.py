@@ -106,6 +106,7 @@ class WindowOutputs:
             "div_pop": torch.zeros(n_win * np_, **f64), "nhaps": torch.zeros(n_win * np_, **i32),
             "hap_val": torch.zeros(n_win * np_, **f64), "hap_dxy": torch.zeros(n_win * npairs, **f64),
             "hap_min": torch.zeros(n_win * npairs, **i32),
+            "tree_diff": torch.zeros(n_win * (n + 1) * (n + 1), **i32),
         }
 
     def struct(self, fields) -> _lib.PbgWindowOut:
@@ -140,6 +141,8 @@ class HotPath:
             fields += ["div_fixed", "div_seg", "div_pop"]
         if stats & (_lib.PBG_S_HAP_K | _lib.PBG_S_HAP_EHHS | _lib.PBG_S_HAP_DXY):
             fields += ["nhaps", "hap_val", "hap_dxy", "hap_min"]
+        if stats & _lib.PBG_S_TREE:
+            fields += ["tree_diff"]
         self.out_struct = self.out.struct(fields)
         self.opts = _lib.PbgStatOpts(stats, min_freq, 0, 0)
         self.pl = synth.pileup()

@@ -15,6 +15,7 @@ For every scenario below this script
 The reference is never needed at test time: tests read the committed fixtures.
 
 Usage:  python tests/golden/make_golden.py [case ...]
+        python tests/golden/make_golden.py --append [case ...]   (new commands only)
 """
 from __future__ import annotations
 
@@ -65,13 +66,15 @@ SCENARIOS = {
     "g01_base": dict(seed=101, L=30000, samples=_samples(12, ["popA", "popB"]), step=10,
                      mu=0.02, cmds=_std_cmds("1", [["nucdiv", "-w", "10"], ["sfs", "-w", "10"],
                                                    ["ld", "-w", "10"], ["nucdiv"], ["sfs"], ["ld"],
-                                                   ["nucdiv", "-w", "2", "-k", "500"]])),
+                                                   ["nucdiv", "-w", "2", "-k", "500"],
+                                                   ["tree", "-w", "1"], ["tree", "-w", "1", "-d", "jc"], ["tree"],
+                                                   ["tree", "-w", "10"], ["tree", "-w", "2", "-k", "500"]])),
     # G2: interleaved population labels (Dxy asymmetry quirk)
     "g02_interleaved": dict(seed=202, L=12000, samples=[(f"s{i}", ["popA", "popB"][i % 2]) for i in range(12)],
                             step=10, mu=0.02, cmds=_std_cmds("1")),
     # G3: three populations
     "g03_threepops": dict(seed=303, L=12000, samples=_samples(12, ["p1", "p2", "p3"]), step=10,
-                          mu=0.03, cmds=_std_cmds("1")),
+                          mu=0.03, cmds=_std_cmds("1") + [["tree", "-w", "1"]]),
     # G4: sfs / diverge / snp with an outgroup flip
     "g04_outgroup": dict(seed=404, L=12000, samples=_samples(12, ["popA", "popB"]), step=10, mu=0.03,
                          cmds=[["sfs", "-w", "1", "-p", "s11"], ["sfs", "-w", "1", "-p", "s0"],
@@ -80,7 +83,8 @@ SCENARIOS = {
     "g05_lowdepth": dict(seed=505, L=12000, samples=_samples(12, ["popA", "popB"]), step=30, mu=0.05,
                          baseq=[12, 15, 18, 20, 22, 25, 30], err=0.03,
                          cmds=_std_cmds("1", [["nucdiv", "-w", "1", "-s", "9"], ["snp", "-s", "9"],
-                                              ["snp", "-m", "2"], ["nucdiv", "-w", "1", "-m", "2"]])),
+                                              ["snp", "-m", "2"], ["nucdiv", "-w", "1", "-m", "2"],
+                                              ["tree", "-w", "1"], ["tree", "-w", "1", "-m", "2", "-s", "9"]])),
     # G6: lowercase soft-masked reference stretch + an N stretch
     "g06_softmask": dict(seed=606, L=12000, samples=_samples(12, ["popA", "popB"]), step=10, mu=0.02,
                          lower=[(3000, 6500)], nrun=[(9000, 9400)], cmds=_std_cmds("1")),
@@ -98,14 +102,14 @@ SCENARIOS = {
     "g09_u16wrap": dict(seed=909, L=300000, samples=_samples(4, ["popA", "popB"]), step=25, mu=0.6,
                         freq_hi=True, baseq=[40], cmds=[["nucdiv", "-m", "2"], ["haplo", "-o", "2", "-m", "2"],
                                                         ["diverge", "-m", "2"], ["diverge", "-o", "1", "-m", "2"],
-                                                        ["nucdiv"]]),
+                                                        ["nucdiv"], ["tree", "-m", "2"], ["tree", "-m", "2", "-d", "jc"]]),
     # G10: deep pileup with -x > 255 (ks_shuffle rotation + truncation to 255 keys)
     "g10_deep": dict(seed=1010, L=2500, samples=_samples(4, ["popA", "popB"]), step=0.2, mu=0.05,
                      read_len=60, cmds=[["nucdiv", "-x", "900"], ["snp", "-x", "900"], ["snp"],
                                         ["nucdiv", "-x", "300", "-m", "280"]]),
     # G11: 11 samples (stand-in for the trial.bam config), 10 kb windows
     "g11_eleven": dict(seed=1111, L=40000, samples=_samples(11, ["mel", "sim"]), step=10, mu=0.015,
-                       cmds=_std_cmds("10")),
+                       cmds=_std_cmds("10") + [["tree", "-w", "10"], ["tree", "-w", "5", "-d", "jc"]]),
     # G12: region forms chr:a-b, chr:a, and windows not aligned to the contig start
     "g12_regions": dict(seed=1212, L=15000, samples=_samples(8, ["popA", "popB"]), step=10, mu=0.03,
                         cmds=[["nucdiv", "REGION=chr1:2001-9000"], ["nucdiv", "-w", "1", "REGION=chr1:1,501-12,000"],
@@ -122,7 +126,8 @@ SCENARIOS = {
                                  ["snp", "-o", "1", "-w", "1", "REGION=chr1:2501-9000"]]),
     # G14: one population (ms header without -I)
     "g14_onepop": dict(seed=1414, L=6000, samples=_samples(6, ["solo"]), step=10, mu=0.03,
-                       cmds=[["snp", "-o", "2"], ["snp", "-o", "2", "-w", "1"], ["snp", "-o", "1"], ["nucdiv", "-w", "1"]]),
+                       cmds=[["snp", "-o", "2"], ["snp", "-o", "2", "-w", "1"], ["snp", "-o", "1"], ["nucdiv", "-w", "1"],
+                             ["tree", "-w", "1"], ["tree", "REGION=chr1:1001-4000"]]),
 }
 
 
@@ -332,9 +337,46 @@ def run_case(name, sc):
             assert np.array_equal(b[k], c[k]), (name, x, k)
 
 
+def append_cases(name, sc):
+    """Run only the commands added to a scenario after its fixtures were made (same BAM,
+    existing outputs untouched; new outputs get the next indices)."""
+    d = os.path.join(HERE, name)
+    with open(os.path.join(d, "meta.json")) as f:
+        meta = json.load(f)
+    for i, cmd in enumerate(sc["cmds"]):
+        if i < len(meta["cases"]):
+            continue
+        region = "chr1"
+        args = []
+        for a in cmd:
+            if a.startswith("REGION="):
+                region = a[len("REGION="):]
+            else:
+                args.append(a)
+        full = [REF_BIN, args[0], "-f", "ref.fa"] + args[1:] + ["in.bam", region]
+        res = subprocess.run(full, cwd=d, capture_output=True, text=True, timeout=600)
+        out = f"out/{i:02d}_{args[0]}.tsv"
+        with open(os.path.join(d, out), "w") as f:
+            f.write(res.stdout)
+        x = int(args[args.index("-x") + 1]) if "-x" in args else 255
+        meta["cases"].append(dict(args=args, region=region, stdout=out, rc=res.returncode,
+                                  max_depth=x, stderr=res.stderr[-400:]))
+        print(f"  {name} {' '.join(args)} {region}: rc={res.returncode} lines={res.stdout.count(chr(10))}")
+    with open(os.path.join(d, "meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    fai = os.path.join(d, "ref.fa.fai")
+    if os.path.exists(fai):
+        os.remove(fai)
+
+
 def main(argv):
     if not os.path.exists(REF_BIN):
         sys.exit("build the reference first: make -C oracle ref")
+    if argv and argv[0] == "--append":
+        for nm in argv[1:] or list(SCENARIOS):
+            print(nm)
+            append_cases(nm, SCENARIOS[nm])
+        return
     names = argv or list(SCENARIOS)
     for nm in names:
         print(nm)

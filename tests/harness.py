@@ -30,7 +30,8 @@ class OrcCmd(C.Structure):
     _fields_ = [("cmd", C.c_int32), ("output", C.c_int32), ("min_sites", C.c_int32), ("min_snps", C.c_int32),
                 ("min_freq", C.c_int32), ("outidx", C.c_int32), ("jc", C.c_int32), ("windowed", C.c_int32),
                 ("win_size", C.c_int64), ("beg", C.c_int32), ("end", C.c_int32), ("chr_name", C.c_char_p),
-                ("sample_names", C.POINTER(C.c_char_p)), ("pop_names", C.POINTER(C.c_char_p))]
+                ("sample_names", C.POINTER(C.c_char_p)), ("pop_names", C.POINTER(C.c_char_p)),
+                ("refid", C.c_char_p)]
 
 
 _orc = None
@@ -79,6 +80,7 @@ class Setup:
         if o.flag & opt.BAM_OUTGROUP:
             self.outidx = max(i for i, s in enumerate(self.sm.samples) if s == o.outgroup)
         self.chr = names[self.tid]
+        self.refid = opt.get_refid(self.case["header"]) if args[0] == "tree" else ""
         self.batch = fixtures.case_batch(case_name, o.max_depth)
 
     def orc_params(self):
@@ -111,6 +113,8 @@ class Setup:
         self._arrs = (sn, pn)
         c.sample_names = C.cast(sn, C.POINTER(C.c_char_p))
         c.pop_names = C.cast(pn, C.POINTER(C.c_char_p))
+        self._refid = self.refid.encode()
+        c.refid = self._refid
         return c
 
 

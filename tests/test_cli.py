@@ -48,7 +48,7 @@ def test_usage_and_unknown_commands(capsys):
     rc, out, err = _main(["frobnicate"], capsys)
     assert rc == 1 and err == "Error: unrecognized command: frobnicate\n"
     rc, out, err = _main(["tree", "x.bam", "chr1"], capsys)
-    assert rc == 1 and "tree" in err
+    assert rc == 1 and "Cannot read BAM file x.bam" in err
 
 
 def test_fatal_errors_before_the_gpu(capsys, tmp_path):
@@ -62,6 +62,8 @@ def test_fatal_errors_before_the_gpu(capsys, tmp_path):
     rc, out, err = _main(["nucdiv", "-f", ref, bam], capsys)
     assert rc == 1 and "Need to specify BAM file name" in err
     rc, out, err = _main(["diverge", "-f", ref, "-d", "kimura", bam, "chr1"], capsys)
+    assert rc == 1 and "kimura is not a valid distance option" in err
+    rc, out, err = _main(["tree", "-f", ref, "-d", "kimura", bam, "chr1"], capsys)
     assert rc == 1 and "kimura is not a valid distance option" in err
     noidx = tmp_path / "in.bam"
     shutil.copy(bam, noidx)

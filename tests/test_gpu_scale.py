@@ -114,6 +114,7 @@ def _window_text(ctx, params, hp, cmd_id, output, windows, min_freq=1, jc=0, min
     pn = (C.c_char_p * np_)(*[f"p{i}".encode() for i in range(np_)])
     c.sample_names = C.cast(sn, C.POINTER(C.c_char_p))
     c.pop_names = C.cast(pn, C.POINTER(C.c_char_p))
+    c.refid = b"ref"
     wb = np.array([a for a, _ in windows], np.int32)
     we = np.array([b for _, b in windows], np.int32)
     cap = 1 << 24
@@ -135,6 +136,7 @@ def _oracle_text(params, types, flags, cmd_id, output, windows, min_freq=1, jc=0
     pn = (C.c_char_p * np_)(*[f"p{i}".encode() for i in range(np_)])
     c.sample_names = C.cast(sn, C.POINTER(C.c_char_p))
     c.pop_names = C.cast(pn, C.POINTER(C.c_char_p))
+    c.refid = b"ref"
     wb = np.array([a for a, _ in windows], np.int32)
     we = np.array([b for _, b in windows], np.int32)
     cap = 1 << 24
@@ -148,7 +150,7 @@ def _oracle_text(params, types, flags, cmd_id, output, windows, min_freq=1, jc=0
 STATS = [  # (PBG_S_* flag, popbam_func_t, -o, min_freq, jc)
     (0x001, 4, 0, 1, 0), (0x002, 6, 0, 1, 0), (0x004, 5, 0, 1, 0), (0x004, 5, 0, 2, 0), (0x008, 5, 1, 1, 0),
     (0x010, 5, 2, 1, 0), (0x020, 2, 0, 1, 0), (0x040, 2, 1, 1, 0), (0x080, 1, 0, 1, 0), (0x100, 1, 1, 1, 0),
-    (0x200, 1, 2, 1, 0),
+    (0x200, 1, 2, 1, 0), (0x400, 3, 0, 1, 0), (0x400, 3, 0, 1, 1),
 ]
 
 
@@ -188,7 +190,8 @@ def test_u16_wrap_and_workspace_window(gpu_lib):
     ctx, params = _ctx(12)
     syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 99)
     wins = [(0, n_sites), (1000, n_sites - 3)]
-    for stat, cmd_id, output in [(0x001, 4, 0), (0x200, 1, 2), (0x020, 2, 0), (0x002, 6, 0), (0x004, 5, 0)]:
+    for stat, cmd_id, output in [(0x001, 4, 0), (0x200, 1, 2), (0x020, 2, 0), (0x002, 6, 0), (0x004, 5, 0),
+                                 (0x400, 3, 0)]:
         hp = workload.HotPath(ctx, syn, wins, stat)
         hp.step()
         torch.cuda.synchronize()
