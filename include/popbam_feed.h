@@ -66,6 +66,16 @@ int  pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refse
                 int n_samples, int max_depth, pbf_batch *out);
 void pbf_batch_free(pbf_batch *batch);
 
+/* pbf_pileup over [beg, end) split into `chunk`-position pieces (rounded up to a multiple of
+ * 64; <= 0 = 1 Mb) walked by `n_threads` threads, each with its own handle on `bam_path`.
+ * A position's pileup depends only on the reads overlapping it, and bam_fetch of a piece
+ * returns all of them in file order, so the merged batch equals one pbf_pileup over the whole
+ * range (the host walk multithreaded by region).  On failure the error is the
+ * one of the first failing piece in position order.                                      */
+int  pbf_pileup_mt(const char *bam_path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
+                   const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
+                   int32_t fallback_sample, int n_samples, int max_depth, pbf_batch *out);
+
 /* fai_fetch: the whole sequence of contig `name` (case preserved, line breaks removed).
  * *seq is malloc'ed (NUL-terminated); free with pbf_free.                                 */
 int  pbf_fasta_fetch(const char *fa_path, const char *name, char **seq, int64_t *len);

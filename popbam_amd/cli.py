@@ -70,7 +70,10 @@ def run(cmd: str, argv: list[str], device: int = 0) -> str:
             seq = seq + b"N" * (end - len(seq))
         fallback = 0 if not sm.rg2sample else -1
         try:
-            batch = bam.pileup(tid, beg, end, seq, sm.rg2sample, sm.n, o.max_depth, fallback)
+            threads = int(os.environ.get("POPBAM_FEED_THREADS", min(8, os.cpu_count() or 1)))
+            chunk = max(1 << 16, -(-(end - beg) // max(1, 4 * threads)))
+            batch = bam.pileup(tid, beg, end, seq, sm.rg2sample, sm.n, o.max_depth, fallback,
+                               threads=threads, chunk=chunk)
         except feed.FeedError as e:
             if e.code == feed.PBF_E_RG:
                 raise opt.PopbamError("Problem assigning read group") from e

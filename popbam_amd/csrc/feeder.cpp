@@ -20,6 +20,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -586,6 +587,74 @@ int pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refseq
         return fail(PBF_E_IO, "out of host memory");
     }
     if (!reads.empty()) memcpy(out->reads, reads.data(), reads.size() * sizeof(uint32_t));
+    return PBF_OK;
+}
+
+int pbf_pileup_mt(const char *path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
+                  const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
+                  int32_t fallback, int ns, int max_depth, pbf_batch *out) {
+    if (!path || !out || !refseq || ns < 1 || end < beg || n_threads < 1) return fail(PBF_E_ARG, "bad argument");
+    memset(out, 0, sizeof(*out));
+    const int64_t L = (int64_t)end - beg;
+    if (chunk <= 0) chunk = 1 << 20;
+    chunk = (chunk + 63) / 64 * 64;   // chunk borders on 64-position blocks: block_off concatenates
+    const int64_t nchunk = std::max<int64_t>(1, (L + chunk - 1) / chunk);
+    std::vector<pbf_batch> parts((size_t)nchunk);
+    std::vector<int> rc((size_t)nchunk, PBF_OK);
+    std::vector<std::string> msg((size_t)nchunk);
+    for (auto &p : parts) memset(&p, 0, sizeof(p));
+    const int nt = (int)std::min<int64_t>(n_threads, nchunk);
+    auto worker = [&](int w) {
+        pbf_bam *b = nullptr;
+        int r = pbf_open(&b, path);
+        for (int64_t c = w; c < nchunk; c += nt) {
+            if (r == PBF_OK) {
+                const int32_t cb = (int32_t)(beg + c * chunk), ce = (int32_t)std::min<int64_t>(end, beg + (c + 1) * chunk);
+                r = pbf_pileup(b, tid, cb, ce, refseq, rg_ids, rg_sample, n_rg, fallback, ns, max_depth, &parts[c]);
+            }
+            rc[c] = r;
+            if (r != PBF_OK) msg[c] = g_err;
+        }
+        if (b) pbf_close(b);
+    };
+    std::vector<std::thread> th;
+    for (int w = 1; w < nt; ++w) th.emplace_back(worker, w);
+    worker(0);
+    for (auto &t : th) t.join();
+    // first failing chunk in position order = the error a sequential walk meets first
+    for (int64_t c = 0; c < nchunk; ++c)
+        if (rc[c] != PBF_OK) {
+            for (auto &p : parts) pbf_batch_free(&p);
+            return fail(rc[c], msg[c]);
+        }
+    uint64_t n_reads = 0;
+    for (auto &p : parts) n_reads += p.n_reads;
+    out->n_sites = (uint32_t)L;
+    out->pos0 = beg;
+    out->n_reads = n_reads;
+    out->ref = (uint8_t *)malloc(std::max<size_t>((size_t)L, 1));
+    out->depth = (uint16_t *)malloc(std::max<size_t>((size_t)L * ns, 1) * sizeof(uint16_t));
+    out->block_off = (uint64_t *)calloc((size_t)L / 64 + 2, sizeof(uint64_t));
+    out->reads = (uint32_t *)malloc(std::max<uint64_t>(n_reads, 1) * sizeof(uint32_t));
+    if (!out->ref || !out->depth || !out->block_off || !out->reads) {
+        for (auto &p : parts) pbf_batch_free(&p);
+        pbf_batch_free(out);
+        return fail(PBF_E_IO, "out of host memory");
+    }
+    size_t site = 0;
+    uint64_t roff = 0;
+    for (auto &p : parts) {
+        if (p.n_sites) {
+            memcpy(out->ref + site, p.ref, p.n_sites);
+            memcpy(out->depth + site * ns, p.depth, (size_t)p.n_sites * ns * sizeof(uint16_t));
+            for (uint32_t bk = 0; bk * 64 < p.n_sites; ++bk) out->block_off[site / 64 + bk] = roff + p.block_off[bk];
+        }
+        if (p.n_reads) memcpy(out->reads + roff, p.reads, p.n_reads * sizeof(uint32_t));
+        site += p.n_sites;
+        roff += p.n_reads;
+        pbf_batch_free(&p);
+    }
+    out->block_off[((size_t)L + 63) / 64] = roff;
     return PBF_OK;
 }
 

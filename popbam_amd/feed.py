@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libpopbam_feed.so")
 
 EXPORTS = ["pbf_last_error", "pbf_open", "pbf_close", "pbf_header_text", "pbf_n_refs", "pbf_ref_name",
-           "pbf_ref_len", "pbf_has_index", "pbf_pileup", "pbf_batch_free", "pbf_fasta_fetch", "pbf_free"]
+           "pbf_ref_len", "pbf_has_index", "pbf_pileup", "pbf_pileup_mt", "pbf_batch_free", "pbf_fasta_fetch", "pbf_free"]
 
 PBF_E_RG = -4
 
@@ -56,6 +56,8 @@ def load():
     lib.pbf_has_index.argtypes = [vp]
     lib.pbf_pileup.argtypes = [vp, C.c_int, C.c_int32, C.c_int32, C.c_char_p, P(C.c_char_p), P(C.c_int32),
                                C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfBatch)]
+    lib.pbf_pileup_mt.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int, C.c_int32, C.c_int32, C.c_char_p,
+                                  P(C.c_char_p), P(C.c_int32), C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfBatch)]
     lib.pbf_batch_free.argtypes = [P(PbfBatch)]
     lib.pbf_batch_free.restype = None
     lib.pbf_fasta_fetch.argtypes = [C.c_char_p, C.c_char_p, P(C.c_void_p), P(C.c_int64)]
@@ -103,23 +105,30 @@ class Bam:
         return bool(self.lib.pbf_has_index(self.h))
 
     def pileup(self, tid: int, beg: int, end: int, refseq: bytes, rg2s: dict, n_samples: int, max_depth: int,
-               fallback_sample: int = -1) -> dict:
+               fallback_sample: int = -1, threads: int = 1, chunk: int = 1 << 20) -> dict:
+        """Dense pileup batch of [beg, end).  threads > 1: pbf_pileup_mt (chunk-position
+        pieces walked in parallel, each thread with its own file handle; same batch)."""
         ids = list(rg2s)
         rg = (C.c_char_p * max(1, len(ids)))(*[i.encode() for i in ids])
         sm = (C.c_int32 * max(1, len(ids)))(*[rg2s[i] for i in ids])
         if len(refseq) < end:
             raise FeedError(-3, "reference sequence shorter than the region")
         out = PbfBatch()
-        _check(self.lib, self.lib.pbf_pileup(self.h, tid, beg, end, refseq, rg, sm, len(ids), fallback_sample,
-                                             n_samples, max_depth, C.byref(out)))
+        if threads > 1:
+            _check(self.lib, self.lib.pbf_pileup_mt(self.path.encode(), threads, chunk, tid, beg, end, refseq, rg, sm,
+                                                    len(ids), fallback_sample, n_samples, max_depth, C.byref(out)))
+        else:
+            _check(self.lib, self.lib.pbf_pileup(self.h, tid, beg, end, refseq, rg, sm, len(ids), fallback_sample,
+                                                 n_samples, max_depth, C.byref(out)))
         try:
             L = out.n_sites
             ref = np.ctypeslib.as_array(out.ref, (max(L, 1),))[:L].copy()
             depth = np.ctypeslib.as_array(out.depth, (max(L * n_samples, 1),))[:L * n_samples].copy()
             reads = np.ctypeslib.as_array(out.reads, (max(out.n_reads, 1),))[:out.n_reads].copy()
+            boff = np.ctypeslib.as_array(out.block_off, ((L + 63) // 64 + 1,)).copy()
         finally:
             self.lib.pbf_batch_free(C.byref(out))
-        return {"ref": ref, "depth": depth.reshape(L, n_samples), "reads": reads, "pos0": beg}
+        return {"ref": ref, "depth": depth.reshape(L, n_samples), "reads": reads, "block_off": boff, "pos0": beg}
 
     def close(self):
         if self.h:

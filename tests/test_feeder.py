@@ -87,3 +87,23 @@ def test_unknown_read_group_is_an_error(tmp_path):
     with pytest.raises(feed.FeedError) as e:
         bam.pileup(0, 0, 2000, c["refseq"], rg2s, sm.n, 255, -1)
     assert e.value.code == feed.PBF_E_RG and "Problem assigning read group" in str(e.value)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_multithreaded_pileup_equals_sequential(name):
+    """pbf_pileup_mt (region pieces walked by several threads, each with its own handle) gives
+    the same batch as one sequential walk, for piece sizes down to one 64-position block and
+    for a region that does not start on a block border."""
+    c = fixtures.load_case(name)
+    bam = feed.Bam(os.path.join(c["dir"], "in.bam"))
+    seq = feed.fasta_fetch(os.path.join(c["dir"], "ref.fa"), bam.refs[0][0])
+    sm = opt.parse_header(bam.header_text, "in.bam")
+    fb = 0 if not sm.rg2sample else -1
+    x = max(cs["max_depth"] for cs in c["meta"]["cases"])
+    for beg, end in [(0, len(seq)), (37, len(seq) - 5)]:
+        one = bam.pileup(0, beg, end, seq, sm.rg2sample, sm.n, x, fb)
+        for threads, chunk in [(4, 64), (3, 1000), (8, 1 << 20)]:
+            mt = bam.pileup(0, beg, end, seq, sm.rg2sample, sm.n, x, fb, threads=threads, chunk=chunk)
+            for k in ("ref", "depth", "reads", "block_off"):
+                assert np.array_equal(one[k], mt[k]), (name, beg, end, threads, chunk, k)
+    bam.close()
