@@ -172,8 +172,10 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (counter-based pileup resident in HBM, generated on device)",
-            "config": {"workload": "configs[2]: synthetic 1 contig x 50 Msites x 12 samples per GPU, "
-                                   "consensus call + nucdiv + sfs + ld(ZnS), 10 kb windows",
+            "config": {"workload": (("configs[2]: " if (args.sites, n, args.window) == (50_000_000, 12, 10_000)
+                                     else "off-metric shape: ") +
+                                    f"synthetic 1 contig x {args.sites / 1e6:g} Msites x {n} samples per GPU, "
+                                    f"consensus call + nucdiv + sfs + ld(ZnS), {args.window / 1e3:g} kb windows"),
                        "sites_per_gpu": args.sites, "samples": n, "mean_depth": args.depth,
                        "window": args.window, "windows_per_gpu": len(wins), "reads_per_gpu": syn.n_reads,
                        "parallelism": f"dp{world} (independent window-range shards, no collective)"},
