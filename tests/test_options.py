@@ -80,3 +80,20 @@ def test_header_tags_searched_past_line_end():
 def test_header_without_read_groups():
     sm = opt.parse_header("@HD\tVN:1.0\n", "x.bam")
     assert sm.samples == ["x.bam"] and sm.pops == ["x.bam"]
+
+
+def test_get_refid():
+    """get_refid (pop_utils.cpp:463-498): first AS: value up to a tab/newline, else fatal."""
+    assert opt.get_refid("@HD\tVN:1.0\n@SQ\tSN:chr1\tLN:9\tAS:dm3\n") == "dm3"
+    assert opt.get_refid("@SQ\tSN:chr1\tAS:ref one\tLN:9\n@SQ\tSN:chr2\tAS:other\n") == "ref one"
+    with pytest.raises(opt.PopbamError, match="AS tag"):
+        opt.get_refid("@SQ\tSN:chr1\tLN:9\n")
+
+
+def test_tree_options():
+    """treeData::parseCommandLine (pop_tree.cpp:590-631): -d pdist|jc, -k, -w in kb."""
+    o = opt.parse_args("tree", ["-f", "r.fa", "-d", "jc", "-w", "5", "-k", "20", "in.bam", "chr1"])
+    assert (o.dist, o.win_size, o.min_sites, o.flag & opt.BAM_WINDOW) == ("jc", 5000, 20, opt.BAM_WINDOW)
+    assert opt.parse_args("tree", ["in.bam", "chr1"]).dist == "pdist"
+    with pytest.raises(opt.PopbamError, match="not a valid distance option"):
+        opt.parse_args("tree", ["-d", "k2p", "in.bam", "chr1"])
