@@ -15,7 +15,8 @@ from popbam_amd import shard
 
 CASES = [("g01_base", ["nucdiv", "-w", "1"], "chr1"), ("g12_regions", ["sfs", "-w", "2"], "chr1:777-14777"),
          ("g11_eleven", ["ld", "-w", "10"], "chr1"), ("g03_threepops", ["diverge", "-w", "1"], "chr1"),
-         ("g12_regions", ["snp"], "chr1:2001-3000"), ("g02_interleaved", ["haplo", "-w", "1", "-o", "2"], "chr1")]
+         ("g12_regions", ["snp"], "chr1:2001-3000"), ("g02_interleaved", ["haplo", "-w", "1", "-o", "2"], "chr1"),
+         ("g01_base", ["tree", "-w", "1", "-d", "jc"], "chr1")]
 
 
 def _windows(beg, end, w, windowed):
@@ -119,7 +120,8 @@ def test_gpu_blocks_on_rebased_pileups(gpu_lib, world):
                 continue
             lo, hi = shard.positions_needed(reg[0], reg[1], st.opts.win_size, windowed)
             sub = shard.slice_batch(st.batch, 0, lo, max(hi, lo + 1))
-            parts.append(engine.run_command(st.opts, st.sm, st.chr, reg[0], reg[1], sub, pos0=sub["pos0"]))
+            parts.append(engine.run_command(st.opts, st.sm, st.chr, reg[0], reg[1], sub, pos0=sub["pos0"],
+                                            refid=st.refid))
         ours = "".join(parts)
         oob = harness.snp_oob_cells(harness.oracle_run(st)) if args[0] == "snp" else None
         ok, diff = harness.same_output(args, harness.oracle_run(st), ours, oob)
