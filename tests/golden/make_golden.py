@@ -128,6 +128,25 @@ SCENARIOS = {
     "g14_onepop": dict(seed=1414, L=6000, samples=_samples(6, ["solo"]), step=10, mu=0.03,
                        cmds=[["snp", "-o", "2"], ["snp", "-o", "2", "-w", "1"], ["snp", "-o", "1"], ["nucdiv", "-w", "1"],
                              ["tree", "-w", "1"], ["tree", "REGION=chr1:1001-4000"]]),
+    # G15: 24 samples in 3 populations (configs[3]'s sample count: 4-byte rows, r^2 tables of
+    # 3 x 9^3 entries; 1 kb and 10 kb windows)
+    "g15_24s3p": dict(seed=1515, L=25000, samples=_samples(24, ["pa", "pb", "pc"]), step=10, mu=0.03,
+                      cmds=_std_cmds("1", [["nucdiv", "-w", "10"], ["sfs", "-w", "10"], ["ld", "-w", "10"],
+                                           ["ld", "-w", "10", "-o", "1"], ["ld", "-w", "10", "-o", "2"],
+                                           ["diverge", "-w", "10"], ["diverge", "-w", "10", "-o", "1"],
+                                           ["haplo", "-w", "10", "-o", "1"], ["sfs", "-w", "1", "-p", "s23"],
+                                           ["tree", "-w", "5"], ["snp", "-o", "1", "-w", "1"], ["snp", "-o", "2", "-w", "2"]])),
+    # G16: 24 samples in 2 populations (r^2 tables 2 x 13^3 = 4394 doubles: beyond the LDS copy)
+    "g16_24s2p": dict(seed=1616, L=20000, samples=_samples(24, ["popA", "popB"]), step=10, mu=0.03,
+                      cmds=_std_cmds("1", [["nucdiv", "-w", "10"], ["sfs", "-w", "10"], ["ld", "-w", "10"],
+                                           ["ld", "-w", "10", "-e"], ["ld", "-w", "10", "-o", "1"]])),
+    # G17: 48 samples in 2 populations (8-byte rows)
+    "g17_48s": dict(seed=1717, L=10000, samples=_samples(48, ["popA", "popB"]), step=10, mu=0.03,
+                    cmds=_std_cmds("1", [["nucdiv", "-w", "5"], ["ld", "-w", "5"], ["tree", "-w", "2"]])),
+    # G18: 64 samples in 4 populations (16-byte rows; the reference's sample limit)
+    "g18_64s4p": dict(seed=1818, L=8000, samples=_samples(64, ["q1", "q2", "q3", "q4"]), step=10, mu=0.03,
+                      cmds=_std_cmds("1", [["nucdiv", "-w", "4"], ["sfs", "-w", "4"], ["ld", "-w", "4"],
+                                           ["haplo", "-w", "2", "-o", "2"]])),
 }
 
 

@@ -14,10 +14,15 @@ pytestmark = pytest.mark.gpu
 SEED = 0xC0FFEE02
 
 
-def _ctx(n, **kw):
+def _ctx(n, n_pops=2, **kw):
     from popbam_amd import _lib, workload
-    params = workload.default_params(n, **kw)
+    params = workload.default_params(n, n_pops, **kw)
     return _lib.Context(params, 0), params
+
+
+# (samples, populations): every row width (2 / 4 / 8 / 16 bytes, both ends of each width)
+# and the r^2 table sizes that leave the LDS copy (2 x 13^3 > 4096 doubles at 24 samples)
+SHAPES = [(12, 2), (24, 2), (24, 3), (30, 3), (48, 2), (62, 2), (64, 4)]
 
 
 def test_synthetic_generator_matches_oracle(gpu_lib):
@@ -154,14 +159,17 @@ STATS = [  # (PBG_S_* flag, popbam_func_t, -o, min_freq, jc)
 ]
 
 
+@pytest.mark.parametrize("n,npops", SHAPES, ids=[f"n{a}p{b}" for a, b in SHAPES])
 @pytest.mark.parametrize("layout", ["ref10kb", "overlap", "ragged"])
 @pytest.mark.parametrize("stat,cmd_id,output,min_freq,jc", STATS)
-def test_window_stats_match_oracle(gpu_lib, layout, stat, cmd_id, output, min_freq, jc):
+def test_window_stats_match_oracle(gpu_lib, n, npops, layout, stat, cmd_id, output, min_freq, jc):
     import torch
     from popbam_amd import workload
     n_sites = 64 * 8000 if stat != 0x008 else 64 * 1600      # omega_max is O(S^3) on the oracle
-    ctx, params = _ctx(12)
-    syn = workload.SynthPileup(ctx, n_sites, 10, SEED)
+    if n > 30:
+        n_sites //= 2
+    ctx, params = _ctx(n, npops)
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + n)
     if layout == "ref10kb":
         wins = workload.reference_windows(0, n_sites, 10_000)
     elif layout == "overlap":
@@ -181,13 +189,14 @@ def test_window_stats_match_oracle(gpu_lib, layout, stat, cmd_id, output, min_fr
     ctx.close()
 
 
-def test_u16_wrap_and_workspace_window(gpu_lib):
+@pytest.mark.parametrize("n,npops", [(12, 2), (24, 3), (64, 4)])
+def test_u16_wrap_and_workspace_window(gpu_lib, n, npops):
     """One window over 1.28 M positions: ~25 k segregating sites (beyond LDS -> global
     workspace) and > 65535 differences per pair for some pairs at high theta."""
     import torch
     from popbam_amd import _lib, workload
     n_sites = 64 * 20000
-    ctx, params = _ctx(12)
+    ctx, params = _ctx(n, npops)
     syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 99)
     wins = [(0, n_sites), (1000, n_sites - 3)]
     for stat, cmd_id, output in [(0x001, 4, 0), (0x200, 1, 2), (0x020, 2, 0), (0x002, 6, 0), (0x004, 5, 0),
