@@ -30,6 +30,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 METRIC = "Msites/sec (nucdiv+sfs+ld, 10kb win, 12 samples) at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+LAYOUT = "keys16"       # pileup batch layout the committed PMC profile was taken on
 
 
 def parse():
@@ -144,12 +145,15 @@ def main():
     stats_ms = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
     kt, kn = C.c_double(0.0), C.c_uint32(0)
     ctx.check(ctx.lib.pbg_kernel_time(ctx.h, C.byref(kt), C.byref(kn)), "pbg_kernel_time")
-    ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
     scan_ms = kt.value / max(1, kn.value)
     total_sites = args.sites * world * args.steps
     value = total_sites / elapsed / 1e6
-    call_bytes = syn.bytes_read_by_call()
-    scan_bytes = syn.bytes_scan_kernel()
+    ct, cn = C.c_double(0.0), C.c_uint32(0)
+    ctx.check(ctx.lib.pbg_call_time(ctx.h, C.byref(ct), C.byref(cn)), "pbg_call_time")
+    call_lib_ms = ct.value / max(1, cn.value)
+    call_bytes = syn.survey_bytes()          # sum(2k + 5) + 1 + row_bytes per position
+    scan_bytes = call_bytes
+    layout_bytes = syn.layout_bytes_scan()
     achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
     stats_bytes = args.sites * ctx.row_bytes
 
@@ -160,7 +164,8 @@ def main():
         try:
             with open(pmc) as f:
                 d = json.load(f)
-            if d.get("sites") == args.sites and d.get("samples") == n and d.get("depth") == args.depth:
+            if (d.get("sites") == args.sites and d.get("samples") == n and d.get("depth") == args.depth
+                    and d.get("layout") == LAYOUT):
                 traffic = d.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -177,13 +182,17 @@ def main():
                                     f"synthetic 1 contig x {args.sites / 1e6:g} Msites x {n} samples per GPU, "
                                     f"consensus call + nucdiv + sfs + ld(ZnS), {args.window / 1e3:g} kb windows"),
                        "sites_per_gpu": args.sites, "samples": n, "mean_depth": args.depth,
-                       "window": args.window, "windows_per_gpu": len(wins), "reads_per_gpu": syn.n_reads,
+                       "window": args.window, "windows_per_gpu": len(wins), "keys_per_gpu": syn.n_keys,
                        "parallelism": f"dp{world} (independent window-range shards, no collective)"},
             "roofline": {"bound": "hbm", "kernel": "call_scan_kernel", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "bytes_per_launch": scan_bytes, "ms_per_launch": round(scan_ms, 4)},
-            "call_stage": {"ms_per_step": round(call_ms, 4), "bytes": call_bytes,
-                           "GBps": round(call_bytes / (call_ms * 1e-3) / 1e9, 2),
+                         "traffic": traffic, "bytes_per_launch": scan_bytes, "ms_per_launch": round(scan_ms, 4),
+                         "bytes_basis": "SURVEY 8(d): sum over (position, sample) of 2k+5, +1 +row_bytes per position",
+                         "layout_bytes_per_launch": layout_bytes,
+                         "frac_layout": round(layout_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "call_stage": {"ms_per_step": round(call_ms, 4), "ms_library_events": round(call_lib_ms, 4),
+                           "bytes": call_bytes, "GBps": round(call_bytes / (call_lib_ms * 1e-3) / 1e9, 2),
+                           "frac": round(call_bytes / (call_lib_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "kernels": "call_scan + call_slow + call_deepq + call_overflow + call_fold"},
             "window_stats": {"ms_per_launch": round(stats_ms, 4), "rows_bytes": stats_bytes,
                              "GBps": round(stats_bytes / (stats_ms * 1e-3) / 1e9, 2),
@@ -194,6 +203,7 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
     ctx.close()
     if dist:
         dist.destroy_process_group()

@@ -14,6 +14,9 @@
  *     falls back to the file-name sample, else the reference's fatal error), first
  *     max_depth reads per sample in pileup order;
  *   - faidx.c fai_fetch of one contig (faidx.c:291; .fai used when present).
+ *   - call_base's per-read loop (popbam.cpp:252-287): baseQ (Illumina offset) / mapQ / N
+ *     filters, the key qq<<5 | strand<<4 | base, k and sum of mapQ^2 -> the pbg_pileup layout
+ *     (pbf_pack, pbf_pileup_keys_mt).
  * Host memory only; no GPU.  Functions return 0 / a non-negative value on success and a
  * negative PBF_E* code on error (message in pbf_last_error()); nothing exits.
  */
@@ -45,6 +48,25 @@ typedef struct {
     uint64_t  n_reads;
 } pbf_batch;
 
+/* the same batch after call_base's per-read loop, laid out as pbg_pileup */
+typedef struct {
+    uint32_t  n_sites;
+    int32_t   pos0;
+    uint8_t  *ref;         /* [n_sites]                                                    */
+    void     *k;           /* [n_sites * n_samples] u8 or u16 (pbf_filter.k_bytes)          */
+    uint32_t *rmsq;        /* [n_sites * n_samples] sum of mapQ^2 over the kept reads       */
+    uint64_t *block_off;   /* [n_sites/64 + 2] keys before each 64-position block           */
+    uint16_t *keys;        /* [n_keys] qq<<5 | strand<<4 | base (16-byte aligned)           */
+    uint64_t  n_keys;
+} pbf_keys;
+
+/* call_base's per-read filters (popbamData members, popbam.h:236-264) */
+typedef struct {
+    int32_t min_baseQ, min_mapQ;   /* -b / -a as the reference holds them (unsigned char)     */
+    int32_t illumina;              /* BAM_ILLUMINA (-i): baseQ > 31 ? baseQ - 31 : 0          */
+    int32_t k_bytes;               /* width of k[]: 1 (max_depth <= 255) or 2 (pbg_k_bytes)   */
+} pbf_filter;
+
 const char *pbf_last_error(void);   /* thread-local */
 
 /* Opens a BAM file and, if present, its index (<path>.bai).  */
@@ -75,6 +97,19 @@ void pbf_batch_free(pbf_batch *batch);
 int  pbf_pileup_mt(const char *bam_path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
                    const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
                    int32_t fallback_sample, int n_samples, int max_depth, pbf_batch *out);
+
+/* call_base's per-read loop (popbam.cpp:252-287) over a raw batch: keeps a read iff
+ * baseQ (after the Illumina offset) >= min_baseQ, mapQ >= min_mapQ and its base is A/C/G/T,
+ * in pileup order.  Arrays allocated by the library; release with pbf_keys_free.          */
+int  pbf_pack(const pbf_batch *raw, int n_samples, const pbf_filter *f, pbf_keys *out);
+void pbf_keys_free(pbf_keys *keys);
+
+/* pbf_pileup_mt + pbf_pack: each thread packs its own pieces, so the raw reads of the whole
+ * region are never held at once.  Same batch as pbf_pack(pbf_pileup_mt(...)).            */
+int  pbf_pileup_keys_mt(const char *bam_path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
+                        const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
+                        int32_t fallback_sample, int n_samples, int max_depth, const pbf_filter *f,
+                        pbf_keys *out);
 
 /* fai_fetch: the whole sequence of contig `name` (case preserved, line breaks removed).
  * *seq is malloc'ed (NUL-terminated); free with pbf_free.                                 */

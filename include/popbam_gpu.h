@@ -8,13 +8,16 @@
  * popbamData::call_base (popbam.cpp:186-313) + clean_heterozygotes / segbase / qfilter
  * (pop_utils.cpp:102-201) per position and then calc_<stat> / print_<stat> per window.
  *
- * This library replaces everything after the callback's per-sample partition:
- *   - the host side of the callback (reference popbam.cpp:220-249: skip is_del /
- *     is_refskip / BAM_FUNMAP, RG -> sample, keep the first max_depth reads per sample)
- *     copies four bytes per kept read out of bam1_t into a dense pileup batch (pbg_pileup);
- *   - pbg_call_sites()     = call_base from popbam.cpp:252 on + clean_heterozygotes +
- *                            segbase + qfilter + cal_site_type + the make_<cmd> site store,
- *                            producing one packed row per position;
+ * This library replaces everything after call_base's per-read loop:
+ *   - the host side of the callback (reference popbam.cpp:220-287: skip is_del /
+ *     is_refskip / BAM_FUNMAP, RG -> sample, keep the first max_depth reads per sample, then
+ *     per read the baseQ / mapQ / N filters and the key qq<<5 | strand<<4 | base, plus the
+ *     sum of mapQ^2) fills a pileup batch (pbg_pileup) with exactly the bytes SURVEY 8(d)
+ *     counts: a u16 key per kept read, per (position, sample) the key count k (u8) and
+ *     sum mapQ^2 (u32), per position the reference byte (libpopbam_feed.so does this);
+ *   - pbg_call_sites()     = call_base from errmod_cal on (popbam.cpp:288-306) +
+ *                            clean_heterozygotes + segbase + qfilter + cal_site_type + the
+ *                            make_<cmd> site store, producing one packed row per position;
  *   - pbg_window_stats()   = calc_diff_matrix + calc_nucdiv / calc_sfs / calc_zns /
  *                            calc_omegamax / calc_wall / calc_diverge / calc_nhaps /
  *                            calc_ehhs / calc_minDxy over any list of windows;
@@ -25,7 +28,8 @@
  * exits; pbg_last_error() has the message.  One context per device; calls on one context are
  * not thread-safe.  Pointers documented "device" must be device (HBM) memory; the caller owns
  * all buffers it passes; the context owns its tables and scratch.  `stream` is a hipStream_t
- * (NULL = default stream); asynchronous entry points only enqueue work on it.
+ * (NULL = default stream); asynchronous entry points only enqueue work on it, and errors the
+ * kernels detect (an inconsistent batch) are reported by the next pbg_check() on that stream.
  */
 #ifndef POPBAM_GPU_H
 #define POPBAM_GPU_H
@@ -36,7 +40,7 @@ extern "C" {
 #endif
 
 #define PBG_MAX_SAMPLES 64     /* u64 masks, as the reference (popbam.1:507-510)        */
-#define PBG_MAX_POPS    16
+#define PBG_MAX_POPS    64     /* pop_mask[] is indexed by population (popbam.1:507-510) */
 #define PBG_SITE_BLOCK  64     /* positions per pbg_pileup.block_off entry                 */
 
 #define PBG_OK           0
@@ -45,6 +49,7 @@ extern "C" {
 #define PBG_E_NOMEM     -3
 #define PBG_E_RANGE     -4
 #define PBG_E_NODEV     -5
+#define PBG_E_BATCH     -6     /* a kernel found block_off inconsistent with k[] (pbg_check) */
 
 /* BAM_* option bits, same values as popbam.h:59-94 */
 #define PBG_F_ILLUMINA     0x02
@@ -63,27 +68,34 @@ typedef struct {
     int32_t  pop_n[PBG_MAX_POPS];       /* pop_nsmpl                                      */
     int32_t  min_depth, max_depth;      /* -m -x                                          */
     int32_t  min_rmsQ, min_snpQ;        /* -q -s                                          */
-    int32_t  min_mapQ, min_baseQ;       /* -a -b (unsigned char in the reference)         */
+    int32_t  min_mapQ, min_baseQ;       /* -a -b (unsigned char in the reference); applied
+                                           by the host when it builds the keys            */
     uint32_t flag;                      /* PBG_F_* bits                                   */
 } pbg_params;
 
-/* Dense pileup batch for contiguous positions [pos0, pos0 + n_sites) of one contig.
- * All pointers are DEVICE pointers.
+/* Dense pileup batch for contiguous positions [pos0, pos0 + n_sites) of one contig, in the
+ * layout SURVEY 8(d) prices (sum over (position, sample) of 2k + 5 bytes, + 1 per position).
+ * All pointers are DEVICE pointers for pbg_call_sites, HOST pointers for pbg_run.
  *   ref[i]        reference base byte (faidx_fetch_seq); bit 7 set = the pileup made no
  *                 callback at this position (no mask-passing read covers it)
- *   depth[i*n+s]  kept reads of sample s at position i (after the max_depth cap)
- *   block_off[b]  index in reads[] of the first read of position b*PBG_SITE_BLOCK;
- *                 ceil(n_sites/PBG_SITE_BLOCK)+1 entries, last = total reads
- *   reads[]       one u32 per kept read, (position, sample, pileup order) major:
- *                 bits 0-7 bam1_qual()[qpos], 8-15 core.qual (mapQ),
- *                 16-19 bam1_seqi(seq, qpos) (nt16), bit 20 bam1_strand()            */
+ *   k[i*n+s]      keys kept for sample s at position i: call_base's `k` after the max_depth
+ *                 cap and the per-read filters (popbam.cpp:266-287); u8 when the context's
+ *                 max_depth <= 255, else u16 (pbg_k_bytes)
+ *   rmsq[i*n+s]   sum of mapQ^2 over those reads (popbam.cpp:287 `rmsq`)
+ *   block_off[b]  index in keys[] of the first key of position b*PBG_SITE_BLOCK;
+ *                 ceil(n_sites/PBG_SITE_BLOCK)+1 entries, last = total keys (pbg_run derives
+ *                 it from k[] when NULL)
+ *   keys[]        one u16 per kept read, (position, sample, pileup order) major:
+ *                 qq<<5 | strand<<4 | base (popbam.cpp:284), qq = clamp(min(baseQ, mapQ), 4, 63)
+ * Device batches: keys[] must be 16-byte aligned (any hipMalloc / torch allocation is).   */
 typedef struct {
     uint32_t        n_sites;
     int32_t         pos0;
     const uint8_t  *ref;
-    const uint16_t *depth;
+    const void     *k;
+    const uint32_t *rmsq;
     const uint64_t *block_off;
-    const uint32_t *reads;
+    const uint16_t *keys;
 } pbg_pileup;
 
 /* Row format written by pbg_call_sites: one little-endian word of W = 8*pbg_row_bytes()
@@ -138,6 +150,13 @@ typedef struct {
     int32_t  *tree_diff;   /* [n_win*(n+1)*(n+1)]       tree diff_matrix (u16 values): taxon 0
                               = the reference (differences = derived count), taxon i+1 =
                               sample i; the neighbour-joining tree is built on the host      */
+    /* Not printed by the reference (SURVEY 8(c) "parity unpinned"; north_star asks for them),
+     * computed under PBG_S_SFS from calc_sfs's own integers (pop_sfs.cpp:227-240):           */
+    int32_t  *sfs_bins;    /* [n_win*n_pops*pbg_sfs_stride()] sfs[j] = segregating sites whose
+                              (outgroup-flipped) derived count in the population is j        */
+    int32_t  *seg_pop;     /* [n_win*n_pops] S of calc_sfs: sites with 0 < freq < n_pop   */
+    double   *theta_w;     /* [n_win*n_pops] Watterson's theta S / a1[n_pop] (a1 of
+                              calc_a1, pop_sfs.cpp:511-525), per window (not per site)      */
 } pbg_window_out;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -145,6 +164,8 @@ int         pbg_create(pbg_ctx **ctx, int device, const pbg_params *params);
 void        pbg_destroy(pbg_ctx *ctx);
 const char *pbg_last_error(const pbg_ctx *ctx);   /* ctx may be NULL (last create error)  */
 int         pbg_row_bytes(const pbg_ctx *ctx);
+int         pbg_k_bytes(const pbg_ctx *ctx);      /* 1 (max_depth <= 255) or 2           */
+int         pbg_sfs_stride(const pbg_ctx *ctx);   /* largest population size + 1          */
 int         pbg_device_count(void);
 
 /* ---- hot path --------------------------------------------------------------------- */
@@ -160,6 +181,11 @@ int pbg_call_sites(pbg_ctx *ctx, const pbg_pileup *pileup, void *rows, uint64_t 
 int pbg_window_stats(pbg_ctx *ctx, const void *rows, uint32_t n_rows, const pbg_window *wins,
                      uint32_t n_win, const pbg_stat_opts *opts, const pbg_window_out *out,
                      void *stream);
+
+/* Waits for `stream` and reports what the kernels flagged since the last check: PBG_OK, or
+ * PBG_E_BATCH when a pileup batch's block_off disagreed with its k[] (the affected blocks
+ * were written as uncounted rows and never read past their key range). */
+int pbg_check(pbg_ctx *ctx, void *stream);
 
 /* ---- one subcommand end to end ------------------------------------------------------ */
 enum { PBG_CMD_SNP = 0, PBG_CMD_HAPLO = 1, PBG_CMD_DIVERGE = 2, PBG_CMD_TREE = 3,
@@ -181,14 +207,20 @@ typedef struct {
     const char *const *pop_names;
     const char *refid;     /* tree: taxon name of the reference (get_refid, pop_utils.cpp:463-498:
                               the header's first AS: tag value)                              */
+    int32_t  ms_windows;   /* snp -o 2 header (print_ms, pop_snp.cpp:114-115, printed before the
+                              first window): 0 = this call's window count; > 0 = print it with
+                              this total (a block of a longer run that starts the run);
+                              < 0 = no header (a later block of a longer run)                */
 } pbg_cmd;
 
 /* Runs `popbam <cmd>` over a HOST pileup batch that covers contig positions
  * [pileup->pos0, pileup->pos0 + n_sites) (host pointers; block_off may be NULL and is then
- * derived from depth[]).  Writes the reference's stdout (TSV) into out (NUL-terminated).
- * Returns the text length, or PBG_E_RANGE with *needed set when cap is too small.        */
+ * derived from k[]).  Writes the reference's stdout (TSV) into out (NUL-terminated).
+ * Returns the text length, or PBG_E_RANGE with *needed set when cap is too small; the text
+ * is then kept by the context and pbg_take_text() copies it without running again.       */
 long pbg_run(pbg_ctx *ctx, const pbg_cmd *cmd, const pbg_pileup *host_pileup, char *out,
              size_t cap, size_t *needed);
+long pbg_take_text(pbg_ctx *ctx, char *out, size_t cap);
 
 /* print_<stat> for windows whose results were copied to the HOST: `host_out` holds host
  * arrays laid out as pbg_window_out, `wbeg`/`wend` the contig coordinates the reference
@@ -199,22 +231,37 @@ long pbg_format(const pbg_ctx *ctx, const pbg_cmd *cmd, const pbg_window_out *ho
 /* ---- profiling ---------------------------------------------------------------------- */
 /* With timing on, every pbg_call_sites records a pair of HIP events on its stream around its
  * dominant kernel (the scan kernel of the rows-only pipeline, the block kernel when
- * consensus words are requested); pbg_kernel_time waits for the recorded events and returns
- * the summed elapsed milliseconds and the number of calls timed.  Turning timing on (again)
- * restarts the count.  No reference counterpart (the reference has no timers).    */
+ * consensus words are requested) and one pair around the whole call; pbg_kernel_time waits
+ * for the recorded events and returns the summed elapsed milliseconds of each and the number
+ * of calls timed.  Turning timing on (again) restarts the count.  No reference counterpart
+ * (the reference has no timers).                                                  */
 int pbg_set_kernel_timing(pbg_ctx *ctx, int on);
 int pbg_kernel_time(pbg_ctx *ctx, double *ms_total, uint32_t *launches);
+int pbg_call_time(pbg_ctx *ctx, double *ms_total, uint32_t *launches);
 
 /* ---- synthetic workload (benchmark) ------------------------------------------------- */
-/* Counter-based pileup generator (splitmix64 keyed on (seed, position)), written straight
- * into device memory: pbg_synth_depth() fills ref/depth/block_off and reports the read
- * count so the caller can allocate `reads` for pbg_synth_reads().  Device pointers.                  */
-int pbg_synth_depth(pbg_ctx *ctx, uint64_t seed, int32_t mean_depth, uint32_t n_sites,
-                    uint8_t *ref, uint16_t *depth, uint64_t *block_off, uint64_t *n_reads,
-                    void *stream);
-int pbg_synth_reads(pbg_ctx *ctx, uint64_t seed, int32_t mean_depth, uint32_t n_sites,
-                    const uint16_t *depth, const uint64_t *block_off, uint32_t *reads,
-                    void *stream);
+/* Counter-based pileup generator (splitmix64 keyed on (seed, contig, position);
+ * depth ~ Binomial(2 * mean_depth, 1/2), baseQ 20..40, mapQ 60, ~0.8 % error bases, theta
+ * ~1.2 %), written straight into device memory in the pbg_pileup layout with the context's
+ * filters applied (the keys the host side of the callback would have built).  Positions
+ * [pos0, pos0 + n_sites) of `contig`; block_off is relative to this batch.                  */
+typedef struct {
+    uint64_t seed;
+    int32_t  contig;
+    int32_t  mean_depth;   /* 1..32                                                       */
+    int64_t  pos0;
+    uint32_t n_sites;
+} pbg_synth_spec;
+
+/* Upper bound on the keys of a batch (n_sites * n * 2 * mean_depth): a keys[] buffer this
+ * large lets pbg_synth_pileup run without any host synchronisation.                       */
+uint64_t pbg_synth_max_keys(const pbg_ctx *ctx, const pbg_synth_spec *spec);
+/* Fills ref / k / rmsq / block_off / keys (device).  keys_cap = capacity of keys[] in keys;
+ * a batch that needs more fails at the next pbg_check (PBG_E_BATCH) with no write past it.
+ * keys = NULL (keys_cap 0) fills everything but the keys (a counting pass).  n_keys (host,
+ * may be NULL) receives the key count and makes the call synchronous.                     */
+int pbg_synth_pileup(pbg_ctx *ctx, const pbg_synth_spec *spec, uint8_t *ref, void *k, uint32_t *rmsq,
+                     uint64_t *block_off, uint16_t *keys, uint64_t keys_cap, uint64_t *n_keys, void *stream);
 
 #ifdef __cplusplus
 }

@@ -1122,9 +1122,10 @@ uint64_t sm64(uint64_t x) {
 }
 }  // namespace
 
-extern "C" void orc_synth_site(uint64_t seed, uint64_t pos, int32_t n, int32_t mean_depth, uint8_t *ref,
-                               uint16_t *depth, uint32_t *reads, uint32_t *n_reads_out) {
-    uint64_t h = sm64(seed ^ sm64(pos));
+extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int32_t n, int32_t mean_depth,
+                               int32_t max_depth, uint8_t *ref, uint16_t *depth, uint32_t *reads,
+                               uint32_t *n_reads_out) {
+    uint64_t h = sm64(seed ^ sm64(pos ^ ((uint64_t)(uint32_t)contig << 40)));
     int ref_idx = (int)(h & 3);
     int snp = ((h >> 2) & 0x3FF) < 12;
     int alt = (ref_idx + 1 + (int)((h >> 12) % 3)) & 3;
@@ -1137,6 +1138,7 @@ extern "C" void orc_synth_site(uint64_t seed, uint64_t pos, int32_t n, int32_t m
         int nb = 2 * mean_depth;
         uint64_t m = nb >= 64 ? ~0ULL : ((1ULL << nb) - 1);
         int d = __builtin_popcountll(bits & m);
+        if (d > max_depth) d = max_depth;   // call_base keeps the first max_depth reads (popbam.cpp:241-246)
         depth[s] = (uint16_t)d;
         int a0 = (snp && (uint32_t)(hs & 0xFFFF) < f16) ? alt : ref_idx;
         int a1 = (snp && (uint32_t)((hs >> 16) & 0xFFFF) < f16) ? alt : ref_idx;
@@ -1151,4 +1153,18 @@ extern "C" void orc_synth_site(uint64_t seed, uint64_t pos, int32_t n, int32_t m
         }
     }
     *n_reads_out = nr;
+}
+
+// positions [pos_lo, pos_lo + L) as one raw batch; reads[] needs L * n * min(2D, max_depth)
+extern "C" uint64_t orc_synth_batch(uint64_t seed, int32_t contig, uint64_t pos_lo, uint32_t L, int32_t n,
+                                    int32_t mean_depth, int32_t max_depth, uint8_t *ref, uint16_t *depth,
+                                    uint32_t *reads) {
+    uint64_t off = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        uint32_t nr = 0;
+        orc_synth_site(seed, contig, pos_lo + i, n, mean_depth, max_depth, ref + i, depth + (size_t)i * n,
+                       reads + off, &nr);
+        off += nr;
+    }
+    return off;
 }

@@ -14,19 +14,20 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("POPBAM_GPU_LIB") or os.path.join(HERE, "libpopbam_gpu.so")
 
 PBG_MAX_SAMPLES = 64
-PBG_MAX_POPS = 16
+PBG_MAX_POPS = 64
 PBG_SITE_BLOCK = 64
 
-PBG_OK, PBG_E_ARG, PBG_E_HIP, PBG_E_NOMEM, PBG_E_RANGE, PBG_E_NODEV = 0, -1, -2, -3, -4, -5
+PBG_OK, PBG_E_ARG, PBG_E_HIP, PBG_E_NOMEM, PBG_E_RANGE, PBG_E_NODEV, PBG_E_BATCH = 0, -1, -2, -3, -4, -5, -6
 
 PBG_S_NUCDIV, PBG_S_SFS, PBG_S_ZNS, PBG_S_OMEGA, PBG_S_WALL = 0x1, 0x2, 0x4, 0x8, 0x10
 PBG_S_DIV_IND, PBG_S_DIV_POP, PBG_S_HAP_K, PBG_S_HAP_EHHS, PBG_S_HAP_DXY = 0x20, 0x40, 0x80, 0x100, 0x200
 PBG_S_TREE = 0x400
 
 # every symbol include/popbam_gpu.h declares
-EXPORTS = ["pbg_create", "pbg_destroy", "pbg_last_error", "pbg_row_bytes", "pbg_device_count",
-           "pbg_call_sites", "pbg_window_stats", "pbg_run", "pbg_format", "pbg_set_kernel_timing",
-           "pbg_kernel_time", "pbg_synth_depth", "pbg_synth_reads"]
+EXPORTS = ["pbg_create", "pbg_destroy", "pbg_last_error", "pbg_row_bytes", "pbg_k_bytes", "pbg_sfs_stride",
+           "pbg_device_count", "pbg_call_sites", "pbg_window_stats", "pbg_check", "pbg_run", "pbg_take_text",
+           "pbg_format", "pbg_set_kernel_timing", "pbg_kernel_time", "pbg_call_time", "pbg_synth_max_keys",
+           "pbg_synth_pileup"]
 
 
 class PbgParams(C.Structure):
@@ -37,8 +38,13 @@ class PbgParams(C.Structure):
 
 
 class PbgPileup(C.Structure):
-    _fields_ = [("n_sites", C.c_uint32), ("pos0", C.c_int32), ("ref", C.c_void_p), ("depth", C.c_void_p),
-                ("block_off", C.c_void_p), ("reads", C.c_void_p)]
+    _fields_ = [("n_sites", C.c_uint32), ("pos0", C.c_int32), ("ref", C.c_void_p), ("k", C.c_void_p),
+                ("rmsq", C.c_void_p), ("block_off", C.c_void_p), ("keys", C.c_void_p)]
+
+
+class PbgSynthSpec(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("contig", C.c_int32), ("mean_depth", C.c_int32), ("pos0", C.c_int64),
+                ("n_sites", C.c_uint32)]
 
 
 class PbgWindow(C.Structure):
@@ -52,7 +58,8 @@ class PbgStatOpts(C.Structure):
 class PbgWindowOut(C.Structure):
     _fields_ = [(nm, C.c_void_p) for nm in
                 ("num_sites", "segsites", "pi", "dxy", "td", "fwh", "ld_snps", "ld_val", "ld_q", "div_ind",
-                 "div_fixed", "div_seg", "div_pop", "nhaps", "hap_val", "hap_dxy", "hap_min", "tree_diff")]
+                 "div_fixed", "div_seg", "div_pop", "nhaps", "hap_val", "hap_dxy", "hap_min", "tree_diff",
+                 "sfs_bins", "seg_pop", "theta_w")]
 
 
 class PbgCmd(C.Structure):
@@ -60,7 +67,7 @@ class PbgCmd(C.Structure):
                 ("min_freq", C.c_int32), ("outidx", C.c_int32), ("jc", C.c_int32), ("windowed", C.c_int32),
                 ("win_size", C.c_int64), ("beg", C.c_int32), ("end", C.c_int32), ("chr_name", C.c_char_p),
                 ("sample_names", C.POINTER(C.c_char_p)), ("pop_names", C.POINTER(C.c_char_p)),
-                ("refid", C.c_char_p)]
+                ("refid", C.c_char_p), ("ms_windows", C.c_int32)]
 
 
 _lib = None
@@ -90,14 +97,19 @@ def load():
     lib.pbg_destroy.restype = None
     lib.pbg_last_error.argtypes = [vp]
     lib.pbg_last_error.restype = C.c_char_p
-    lib.pbg_row_bytes.argtypes = [vp]
-    lib.pbg_row_bytes.restype = C.c_int
+    for nm in ("pbg_row_bytes", "pbg_k_bytes", "pbg_sfs_stride"):
+        getattr(lib, nm).argtypes = [vp]
+        getattr(lib, nm).restype = C.c_int
     lib.pbg_device_count.argtypes = []
     lib.pbg_device_count.restype = C.c_int
     lib.pbg_call_sites.argtypes = [vp, P(PbgPileup), vp, vp, vp]
     lib.pbg_call_sites.restype = C.c_int
     lib.pbg_window_stats.argtypes = [vp, vp, C.c_uint32, vp, C.c_uint32, P(PbgStatOpts), P(PbgWindowOut), vp]
     lib.pbg_window_stats.restype = C.c_int
+    lib.pbg_check.argtypes = [vp, vp]
+    lib.pbg_check.restype = C.c_int
+    lib.pbg_take_text.argtypes = [vp, C.c_char_p, C.c_size_t]
+    lib.pbg_take_text.restype = C.c_long
     lib.pbg_run.argtypes = [vp, P(PbgCmd), P(PbgPileup), C.c_char_p, C.c_size_t, P(C.c_size_t)]
     lib.pbg_run.restype = C.c_long
     lib.pbg_format.argtypes = [vp, P(PbgCmd), P(PbgWindowOut), C.c_uint32, vp, vp, C.c_char_p, C.c_size_t,
@@ -107,10 +119,12 @@ def load():
     lib.pbg_set_kernel_timing.restype = C.c_int
     lib.pbg_kernel_time.argtypes = [vp, P(C.c_double), P(C.c_uint32)]
     lib.pbg_kernel_time.restype = C.c_int
-    lib.pbg_synth_depth.argtypes = [vp, C.c_uint64, C.c_int32, C.c_uint32, vp, vp, vp, P(C.c_uint64), vp]
-    lib.pbg_synth_depth.restype = C.c_int
-    lib.pbg_synth_reads.argtypes = [vp, C.c_uint64, C.c_int32, C.c_uint32, vp, vp, vp, vp]
-    lib.pbg_synth_reads.restype = C.c_int
+    lib.pbg_call_time.argtypes = [vp, P(C.c_double), P(C.c_uint32)]
+    lib.pbg_call_time.restype = C.c_int
+    lib.pbg_synth_max_keys.argtypes = [vp, P(PbgSynthSpec)]
+    lib.pbg_synth_max_keys.restype = C.c_uint64
+    lib.pbg_synth_pileup.argtypes = [vp, P(PbgSynthSpec), vp, vp, vp, vp, vp, C.c_uint64, P(C.c_uint64), vp]
+    lib.pbg_synth_pileup.restype = C.c_int
     _lib = lib
     return lib
 
@@ -138,6 +152,18 @@ class Context:
     @property
     def row_bytes(self):
         return self.lib.pbg_row_bytes(self.h)
+
+    @property
+    def k_bytes(self):
+        return self.lib.pbg_k_bytes(self.h)
+
+    @property
+    def sfs_stride(self):
+        return self.lib.pbg_sfs_stride(self.h)
+
+    def sync_check(self, stream=None):
+        """pbg_check: wait for `stream` and raise if a kernel flagged an inconsistent batch."""
+        return self.check(self.lib.pbg_check(self.h, stream), "pbg_check")
 
     def close(self):
         if self.h:

@@ -5,8 +5,12 @@ subcommands snp, nucdiv, sfs, ld, diverge, haplo and tree:
   parseCommandLine (GetOpt_pp quirks, options.parse_args)
   -> checkBAM (popbam.cpp:95-143: BAM, optional -h header text, .bai, FASTA)
   -> bam_smpl_add (options.parse_header) -> bam_parse_region (options.parse_region)
-  -> faidx_fetch_seq of the contig -> one pileup of the region (libpopbam_feed.so)
+  -> faidx_fetch_seq of the contig
+  -> per block of whole windows: pileup + per-sample partition + call_base's per-read loop
+     (libpopbam_feed.so, multithreaded; the next block is read while the GPU runs this one)
   -> pbg_run (libpopbam_gpu.so: consensus call, the reference's window loop, print_<cmd>).
+Blocks bound host and device memory by the block, not the region (the reference re-fetches
+every window, pop_nucdiv.cpp:57-125); the text is the concatenation of the blocks' texts.
 stdout is the reference's TSV byte for byte; errors are reported like fatal_error
 (pop_utils.cpp:510-519) with exit status 1.  `tree` (main_tree, pop_tree.cpp:10-136) takes its
 per-window diff_matrix from the GPU and joins the (n+1)-taxon tree on the host.
@@ -40,9 +44,23 @@ def _fatal(msg: str) -> int:
     return 1
 
 
+def window_blocks(beg: int, end: int, win_size: int, windowed: bool, block_sites: int):
+    """Regions (beg', end') whose window loops print, in order, exactly the windows of
+    (beg, end): blocks of whole windows covering about block_sites positions each
+    (popbam_amd.shard's geometry).  Without -w the region is one window, one block."""
+    from . import shard
+    if not windowed:
+        return [(beg, end)]
+    nw = shard.num_windows(beg, end, win_size, True)
+    per = max(1, block_sites // max(1, win_size))
+    return [(beg + a * win_size, beg + min(nw, a + per) * win_size + 1) for a in range(0, nw, per)]
+
+
 def run(cmd: str, argv: list[str], device: int = 0) -> str:
     """One `popbam <cmd> argv...` invocation; returns stdout text (raises PopbamError)."""
-    from . import engine, feed
+    from concurrent.futures import ThreadPoolExecutor
+
+    from . import _lib, engine, feed, shard
 
     o = opt.parse_args(cmd, argv)
     if not os.path.exists(o.bamfile):
@@ -69,16 +87,42 @@ def run(cmd: str, argv: list[str], device: int = 0) -> str:
         if len(seq) < end:   # positions past the contig's sequence: no reference base
             seq = seq + b"N" * (end - len(seq))
         fallback = 0 if not sm.rg2sample else -1
+        windowed = bool(o.flag & opt.BAM_WINDOW)
+        threads = int(os.environ.get("POPBAM_FEED_THREADS", min(8, os.cpu_count() or 1)))
+        blocks = [b for b in window_blocks(beg, end, o.win_size, windowed,
+                                           int(os.environ.get("POPBAM_BLOCK_SITES", 1 << 22)))]
+        flt = engine.make_filter(o)
+
+        def pile(reg):
+            lo, hi = shard.positions_needed(reg[0], reg[1], o.win_size, windowed)
+            chunk = max(1 << 16, -(-(hi - lo) // max(1, 4 * threads)))
+            try:
+                return lo, bam.pileup_keys(tid, lo, hi, seq, sm.rg2sample, sm.n, o.max_depth, flt, fallback,
+                                           threads=threads, chunk=chunk)
+            except feed.FeedError as e:
+                if e.code == feed.PBF_E_RG:
+                    raise opt.PopbamError("Problem assigning read group") from e
+                raise opt.PopbamError(f"Failed to retrieve region {o.region}: {e}") from e
+
+        nw_total = shard.num_windows(beg, end, o.win_size, windowed)
+        if not blocks:   # no window: the reference's loop prints nothing
+            return ""
+        ctx = _lib.Context(engine.make_params(o, sm), device)
+        parts = []
         try:
-            threads = int(os.environ.get("POPBAM_FEED_THREADS", min(8, os.cpu_count() or 1)))
-            chunk = max(1 << 16, -(-(end - beg) // max(1, 4 * threads)))
-            batch = bam.pileup(tid, beg, end, seq, sm.rg2sample, sm.n, o.max_depth, fallback,
-                               threads=threads, chunk=chunk)
-        except feed.FeedError as e:
-            if e.code == feed.PBF_E_RG:
-                raise opt.PopbamError("Problem assigning read group") from e
-            raise opt.PopbamError(f"Failed to retrieve region {o.region}: {e}") from e
-        return engine.run_command(o, sm, names[tid], beg, end, batch, pos0=beg, device=device, refid=refid)
+            with ThreadPoolExecutor(1) as ex:
+                nxt = ex.submit(pile, blocks[0])
+                for i, reg in enumerate(blocks):
+                    lo, batch = nxt.result()
+                    if i + 1 < len(blocks):
+                        nxt = ex.submit(pile, blocks[i + 1])
+                    ms = (nw_total if i == 0 else -1) if len(blocks) > 1 else 0
+                    parts.append(engine.run_command(o, sm, names[tid], reg[0], reg[1], batch, pos0=lo, ctx=ctx,
+                                                    refid=refid, ms_windows=ms))
+                    del batch
+        finally:
+            ctx.close()
+        return "".join(parts)
     finally:
         bam.close()
 

@@ -41,10 +41,16 @@ struct pbg_ctx {
     // samples deeper than the register sort width (call kernel): queues + parked info bytes
     pbg::DeepBufs deep{};
     size_t deep_sites_cap = 0, deep_info_cap = 0;
-    // pbg_set_kernel_timing: HIP events around the dominant call kernel of every call
+    // pbg_set_kernel_timing: HIP events around the dominant call kernel of every call, and
+    // around the whole call
     bool timing = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev, evc;
     size_t ev_used = 0;
+    // pbg_synth_pileup: block-total scan scratch
+    uint64_t *d_synth = nullptr;
+    size_t synth_cap = 0;
+    // pbg_run text kept when the caller's buffer was too small (pbg_take_text)
+    std::string text;
 };
 
 namespace {
@@ -95,13 +101,16 @@ int pbg_device_count(void) {
 const char *pbg_last_error(const pbg_ctx *ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int pbg_row_bytes(const pbg_ctx *ctx) { return ctx ? ctx->row_bytes : 0; }
+int pbg_k_bytes(const pbg_ctx *ctx) { return ctx ? (ctx->dp.k16 ? 2 : 1) : 0; }
+int pbg_sfs_stride(const pbg_ctx *ctx) { return ctx ? ctx->dp.sfs_stride : 0; }
 
 int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     if (!out || !p) return fail(nullptr, PBG_E_ARG, "null argument");
     *out = nullptr;
     if (p->n_samples < 1 || p->n_samples > PBG_MAX_SAMPLES)
         return fail(nullptr, PBG_E_ARG, "n_samples must be in [1, 64] (u64 sample masks, popbam.1:507-510)");
-    if (p->n_pops < 1 || p->n_pops > PBG_MAX_POPS) return fail(nullptr, PBG_E_ARG, "n_pops must be in [1, 16]");
+    if (p->n_pops < 1 || p->n_pops > PBG_MAX_POPS) return fail(nullptr, PBG_E_ARG, "n_pops must be in [1, 64]");
+    if (p->max_depth < 1 || p->max_depth > 65535) return fail(nullptr, PBG_E_ARG, "max_depth must be in [1, 65535]");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return fail(nullptr, PBG_E_NODEV, "no HIP device visible (libpopbam_gpu has no CPU path)");
@@ -124,6 +133,9 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     d.min_mapQ = p->min_mapQ & 0xff;
     d.min_baseQ = p->min_baseQ & 0xff;
     d.flag = p->flag;
+    d.k16 = p->max_depth > 255 ? 1 : 0;
+    d.sfs_stride = 1;
+    for (int i = 0; i < p->n_pops; ++i) d.sfs_stride = std::max(d.sfs_stride, p->pop_n[i] + 1);
     auto bad = [&](hipError_t e, const char *what) {
         std::string m = std::string(what) + ": " + hipGetErrorString(e);
         pbg_destroy(c);
@@ -187,29 +199,32 @@ void pbg_destroy(pbg_ctx *c) {
                     (void *)c->d_fbeta, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
                     (void *)c->deep.blk_cnt, (void *)c->deep.raw,
-                    (void *)c->d_segcnt})
+                    (void *)c->d_segcnt, (void *)c->d_synth})
         if (p) (void)hipFree(p);
-    for (auto &e : c->ev) {
-        (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
-    }
+    for (auto *v : {&c->ev, &c->evc})
+        for (auto &e : *v) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
     delete c;
 }
 
 int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, void *stream) {
     if (!c || !pl || !rows) return fail(c, PBG_E_ARG, "null argument");
     if (pl->n_sites == 0) return PBG_OK;
-    if (!pl->ref || !pl->depth || !pl->block_off || !pl->reads) return fail(c, PBG_E_ARG, "null pileup array");
+    if (!pl->ref || !pl->k || !pl->rmsq || !pl->block_off || !pl->keys) return fail(c, PBG_E_ARG, "null pileup array");
+    if (((uintptr_t)pl->keys & 15) || ((uintptr_t)rows & 15)) return fail(c, PBG_E_ARG, "keys / rows must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
-    // LDS staging capacity: the mean block plus six standard deviations (Poisson-like),
-    // bounded by what one CU can give a workgroup; blocks above it read HBM directly
     const uint32_t nblk = (pl->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
-    if (c->cap_key != (const void *)pl->block_off || c->cap_sites != pl->n_sites) {
+    if (cb && (c->cap_key != (const void *)pl->block_off || c->cap_sites != pl->n_sites)) {
+        // LDS staging capacity of the consensus-word kernel: the mean round plus six standard
+        // deviations (Poisson-like), bounded by what one CU can give a workgroup; rounds above
+        // it read HBM directly
         uint64_t total = 0;
         HIPCHK(c, hipMemcpyAsync(&total, pl->block_off + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost,
                                  (hipStream_t)stream));
         HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
-        // reads staged per round = reads of kBlockThreads consecutive (position, sample) tasks
+        // keys staged per round = keys of kBlockThreads consecutive (position, sample) tasks
         const double mean = (double)total / ((double)pl->n_sites * c->dp.n) * pbg::kBlockThreads;
         uint32_t cap = (uint32_t)(mean + 6.0 * std::sqrt(mean) + 64.0);
         cap = (cap + 63) & ~63u;
@@ -219,8 +234,10 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         c->cap_sites = pl->n_sites;
     }
     const uint32_t cap = c->cap_val;
-    // deep-sample queues: positions (worst case all), parked info bytes (n per position), and a
-    // task queue sized for ~3 % of tasks; overflowing tasks are computed inside the main kernel
+    // queues: positions (worst case all), parked info bytes (n per position), per-block queue
+    // regions of 3/16 of the block's tasks (+32) for the rows-only pipeline (segregating
+    // positions cluster queued tasks; the rest is computed by the overflow kernel); the
+    // consensus-word pipeline's deep queue shares the task array
     if (c->deep_sites_cap < pl->n_sites || c->deep_info_cap < (size_t)pl->n_sites * c->dp.n) {
         for (void *p : {(void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.blk_cnt,
                         (void *)c->deep.raw})
@@ -232,39 +249,54 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         c->deep.info = nullptr;
         c->deep_sites_cap = c->deep_info_cap = 0;
         const size_t ntask = (size_t)pl->n_sites * c->dp.n;
-        const size_t nblk = (pl->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
-        // rows-only calls queue every task that is not reference-only (~10 % at depth 10 with
-        // 1 % errors; segregating positions cluster them) in a per-block region of 3/16 of the
-        // block's tasks (+32); the rest is computed by the overflow kernel.  The cb path's deep
-        // queue shares the array.
         const uint32_t blk_cap = (uint32_t)(pbg::kSiteBlock * c->dp.n * 3 / 16 + 32);
-        const size_t tcap = std::max<size_t>(nblk * blk_cap, std::min<size_t>(ntask / 32 + 65536, 0xFFFFFFFFu));
+        const size_t tcap = std::max<size_t>((size_t)nblk * blk_cap, std::min<size_t>(ntask / 32 + 65536, 0xFFFFFFFFu));
         HIPCHK(c, hipMalloc((void **)&c->deep.sites, (size_t)pl->n_sites * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc((void **)&c->deep.tasks, tcap * sizeof(pbg::DeepTask)));
         HIPCHK(c, hipMalloc((void **)&c->deep.info, ntask));
         c->deep.task_cap = (uint32_t)std::min<size_t>(tcap, 0xFFFFFFFFu);
         c->deep.blk_cap = blk_cap;
-        HIPCHK(c, hipMalloc((void **)&c->deep.blk_cnt, nblk * sizeof(uint32_t)));
-        HIPCHK(c, hipMalloc((void **)&c->deep.raw, nblk * blk_cap * 4 * sizeof(uint4)));
+        HIPCHK(c, hipMalloc((void **)&c->deep.blk_cnt, (size_t)nblk * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc((void **)&c->deep.raw, (size_t)nblk * blk_cap * 2 * sizeof(uint4)));
         c->deep_sites_cap = pl->n_sites;
         c->deep_info_cap = ntask;
     }
     if (!c->deep.count) HIPCHK(c, hipMalloc((void **)&c->deep.count, 4 * sizeof(uint32_t)));
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, c0 = nullptr, c1 = nullptr;
     if (c->timing) {
         if (c->ev_used == c->ev.size()) {
-            hipEvent_t a, b;
+            hipEvent_t a, b, x, y;
             HIPCHK(c, hipEventCreate(&a));
             HIPCHK(c, hipEventCreate(&b));
+            HIPCHK(c, hipEventCreate(&x));
+            HIPCHK(c, hipEventCreate(&y));
             c->ev.emplace_back(a, b);
+            c->evc.emplace_back(x, y);
         }
         e0 = c->ev[c->ev_used].first;
         e1 = c->ev[c->ev_used].second;
+        c0 = c->evc[c->ev_used].first;
+        c1 = c->evc[c->ev_used].second;
         ++c->ev_used;
+        HIPCHK(c, hipEventRecord(c0, (hipStream_t)stream));
     }
-    HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, pl->n_sites, pl->ref, pl->depth, pl->block_off,
-                                     pl->reads, cap, rows, cb, c->d_err, c->deep, (hipStream_t)stream, e0, e1));
+    const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys};
+    HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, B, cap, rows, cb, c->d_err, c->deep,
+                                     (hipStream_t)stream, e0, e1));
+    if (c1) HIPCHK(c, hipEventRecord(c1, (hipStream_t)stream));
     return PBG_OK;
+}
+
+int pbg_check(pbg_ctx *c, void *stream) {
+    if (!c) return fail(c, PBG_E_ARG, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+    int herr = 0;
+    HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (!herr) return PBG_OK;
+    HIPCHK(c, hipMemset(c->d_err, 0, sizeof(int)));
+    if (herr & 2) return fail(c, PBG_E_BATCH, "synthetic batch needs more keys than keys_cap");
+    return fail(c, PBG_E_BATCH, "pileup block_off disagrees with k[]");
 }
 
 int pbg_set_kernel_timing(pbg_ctx *c, int on) {
@@ -282,6 +314,21 @@ int pbg_kernel_time(pbg_ctx *c, double *ms_total, uint32_t *launches) {
         HIPCHK(c, hipEventSynchronize(c->ev[i].second));
         float ms = 0.0f;
         HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i].first, c->ev[i].second));
+        tot += ms;
+    }
+    *ms_total = tot;
+    *launches = (uint32_t)c->ev_used;
+    return PBG_OK;
+}
+
+int pbg_call_time(pbg_ctx *c, double *ms_total, uint32_t *launches) {
+    if (!c || !ms_total || !launches) return fail(c, PBG_E_ARG, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    double tot = 0.0;
+    for (size_t i = 0; i < c->ev_used; ++i) {
+        HIPCHK(c, hipEventSynchronize(c->evc[i].second));
+        float ms = 0.0f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->evc[i].first, c->evc[i].second));
         tot += ms;
     }
     *ms_total = tot;
@@ -365,44 +412,42 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     return PBG_OK;
 }
 
-int pbg_synth_depth(pbg_ctx *c, uint64_t seed, int32_t mean_depth, uint32_t n_sites, uint8_t *ref, uint16_t *depth,
-                    uint64_t *block_off, uint64_t *n_reads, void *stream) {
-    if (!c || !ref || !depth || !block_off) return fail(c, PBG_E_ARG, "null argument");
-    if (mean_depth < 1 || mean_depth > 32) return fail(c, PBG_E_ARG, "mean_depth must be in [1, 32]");
-    HIPCHK(c, hipSetDevice(c->device));
-    hipStream_t s = (hipStream_t)stream;
-    const uint32_t nblk = (n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
-    HIPCHK(c, pbg::launch_synth_depth(seed, mean_depth, c->dp.n, n_sites, ref, depth, block_off, s));
-    // exclusive scan of the per-block totals on the host (one-off generation step)
-    std::vector<uint64_t> t(nblk + 1, 0);
-    HIPCHK(c, hipMemcpyAsync(t.data(), block_off, nblk * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    uint64_t run = 0;
-    for (uint32_t i = 0; i < nblk; ++i) {
-        uint64_t v = t[i];
-        t[i] = run;
-        run += v;
-    }
-    t[nblk] = run;
-    HIPCHK(c, hipMemcpyAsync(block_off, t.data(), (nblk + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    if (n_reads) *n_reads = run;
-    return PBG_OK;
+uint64_t pbg_synth_max_keys(const pbg_ctx *c, const pbg_synth_spec *sp) {
+    if (!c || !sp) return 0;
+    const int dmax = std::min(2 * sp->mean_depth, c->dp.max_depth);
+    return (uint64_t)sp->n_sites * (uint64_t)c->dp.n * (uint64_t)std::max(dmax, 0);
 }
 
-int pbg_synth_reads(pbg_ctx *c, uint64_t seed, int32_t mean_depth, uint32_t n_sites, const uint16_t *depth,
-                    const uint64_t *block_off, uint32_t *reads, void *stream) {
-    if (!c || !depth || !block_off || !reads) return fail(c, PBG_E_ARG, "null argument");
+int pbg_synth_pileup(pbg_ctx *c, const pbg_synth_spec *sp, uint8_t *ref, void *k, uint32_t *rmsq, uint64_t *block_off,
+                     uint16_t *keys, uint64_t keys_cap, uint64_t *n_keys, void *stream) {
+    if (!c || !sp || !ref || !k || !rmsq || !block_off || (!keys && keys_cap)) return fail(c, PBG_E_ARG, "null argument");
+    if (sp->mean_depth < 1 || sp->mean_depth > 32) return fail(c, PBG_E_ARG, "mean_depth must be in [1, 32]");
+    if ((uintptr_t)keys & 15) return fail(c, PBG_E_ARG, "keys must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, pbg::launch_synth_reads(seed, mean_depth, c->dp.n, n_sites, depth, block_off, reads,
-                                      (hipStream_t)stream));
+    hipStream_t s = (hipStream_t)stream;
+    const size_t need = pbg::synth_scratch_words(sp->n_sites) * 8;
+    if (need > c->synth_cap) {
+        if (c->d_synth) HIPCHK(c, hipFree(c->d_synth));
+        c->d_synth = nullptr;
+        HIPCHK(c, hipMalloc((void **)&c->d_synth, need));
+        c->synth_cap = need;
+    }
+    HIPCHK(c, pbg::launch_synth(c->dp, sp->seed, sp->contig, sp->mean_depth, sp->pos0, sp->n_sites, ref, k, rmsq,
+                                block_off, keys, keys_cap, c->d_synth, c->d_err, s));
+    if (n_keys) {
+        const uint32_t nblk = (sp->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
+        HIPCHK(c, hipMemcpyAsync(n_keys, block_off + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        int rc = pbg_check(c, stream);
+        if (rc) return rc;
+    }
     return PBG_OK;
 }
 
 long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, size_t cap, size_t *needed) {
     if (!c || !cmd || !hp || (!out && cap)) return fail(c, PBG_E_ARG, "null argument");
-    if (hp->n_sites && (!hp->ref || !hp->depth || !hp->reads)) return fail(c, PBG_E_ARG, "null pileup array");
+    if (hp->n_sites && (!hp->ref || !hp->k || !hp->rmsq || !hp->keys)) return fail(c, PBG_E_ARG, "null pileup array");
     HIPCHK(c, hipSetDevice(c->device));
+    c->text.clear();
     c->cap_key = nullptr;   // this call's buffers are fresh allocations: drop cached plans
     c->ws_key = nullptr;
     const int n = c->dp.n, np = c->dp.npops;
@@ -429,6 +474,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
     }
     std::vector<uint64_t> boff;
     const uint64_t *hboff = hp->block_off;
+    const int kb = c->dp.k16 ? 2 : 1;
     const uint32_t nblk_all = (hp->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
     if (!hboff) {
         boff.assign(nblk_all + 1, 0);
@@ -436,7 +482,8 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         for (uint32_t b = 0; b < nblk_all; ++b) {
             boff[b] = run;
             const uint32_t s1 = std::min<uint32_t>(hp->n_sites, (b + 1) * pbg::kSiteBlock);
-            for (size_t i = (size_t)b * pbg::kSiteBlock * n; i < (size_t)s1 * n; ++i) run += hp->depth[i];
+            for (size_t i = (size_t)b * pbg::kSiteBlock * n; i < (size_t)s1 * n; ++i)
+                run += kb == 1 ? ((const uint8_t *)hp->k)[i] : ((const uint16_t *)hp->k)[i];
         }
         boff[nblk_all] = run;
         hboff = boff.data();
@@ -451,7 +498,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
     const uint64_t r0 = lo < hi ? hboff[blo] : 0, r1 = lo < hi ? hboff[bhi] : 0;
     const uint32_t dblk = bhi - blo;
 
-    DevBuf d_ref, d_dep, d_boff, d_reads, d_rows, d_cb, d_win;
+    DevBuf d_ref, d_k, d_rq, d_boff, d_keys, d_rows, d_cb, d_win;
     hipStream_t s = nullptr;
     const int rb = c->row_bytes;
     const bool is_snp = cmd->cmd == PBG_CMD_SNP;
@@ -459,24 +506,24 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
     if (dsites) {
         std::vector<uint64_t> lb(dblk + 1);
         for (uint32_t b = 0; b <= dblk; ++b) lb[b] = hboff[blo + b] - r0;
+        const size_t t0 = (size_t)blo * pbg::kSiteBlock * n, nt = (size_t)dsites * n;
         HIPCHK(c, d_ref.alloc(dsites));
-        HIPCHK(c, d_dep.alloc((size_t)dsites * n * 2));
+        HIPCHK(c, d_k.alloc(nt * kb));
+        HIPCHK(c, d_rq.alloc(nt * 4));
         HIPCHK(c, d_boff.alloc((dblk + 1) * 8));
-        HIPCHK(c, d_reads.alloc((r1 - r0) * 4));
+        HIPCHK(c, d_keys.alloc((r1 - r0) * 2));
         HIPCHK(c, d_rows.alloc((size_t)dsites * rb));
         HIPCHK(c, hipMemcpy(d_ref.p, hp->ref + (size_t)blo * pbg::kSiteBlock, dsites, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(d_dep.p, hp->depth + (size_t)blo * pbg::kSiteBlock * n, (size_t)dsites * n * 2,
-                            hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(d_k.p, (const char *)hp->k + t0 * kb, nt * kb, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(d_rq.p, hp->rmsq + t0, nt * 4, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(d_boff.p, lb.data(), (dblk + 1) * 8, hipMemcpyHostToDevice));
-        if (r1 > r0) HIPCHK(c, hipMemcpy(d_reads.p, hp->reads + r0, (r1 - r0) * 4, hipMemcpyHostToDevice));
+        if (r1 > r0) HIPCHK(c, hipMemcpy(d_keys.p, hp->keys + r0, (r1 - r0) * 2, hipMemcpyHostToDevice));
         if (snp_words) HIPCHK(c, d_cb.alloc((size_t)dsites * n * 8));
-        pbg_pileup dp{dsites, (int32_t)dpos0, (const uint8_t *)d_ref.p, (const uint16_t *)d_dep.p,
-                      (const uint64_t *)d_boff.p, (const uint32_t *)d_reads.p};
+        pbg_pileup dp{dsites, (int32_t)dpos0, (const uint8_t *)d_ref.p, d_k.p, (const uint32_t *)d_rq.p,
+                      (const uint64_t *)d_boff.p, (const uint16_t *)d_keys.p};
         int rc = pbg_call_sites(c, &dp, d_rows.p, snp_words ? (uint64_t *)d_cb.p : nullptr, s);
         if (rc) return rc;
-        int herr = 0;
-        HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
-        if (herr) return fail(c, PBG_E_ARG, "pileup block_off disagrees with depth[]");
+        if ((rc = pbg_check(c, s))) return rc;
     }
     std::string text;
     if (is_snp) {
@@ -490,7 +537,10 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
             if (snp_words) HIPCHK(c, hipMemcpy(cb.data(), d_cb.p, cb.size() * 8, hipMemcpyDeviceToHost));
         }
         const uint64_t tmask = n >= 64 ? ~0ULL : (1ULL << n) - 1;
-        if (cmd->output == 2) pbg::format_ms_header(text, n, np, c->params.pop_n, (long)win.size());
+        // print_ms prints its header in the window loop at cw == 0 (pop_snp.cpp:114-115): not at
+        // all without windows; a block of a longer run passes the run's count or suppresses it
+        if (cmd->output == 2 && cmd->ms_windows >= 0 && !win.empty())
+            pbg::format_ms_header(text, n, np, c->params.pop_n, cmd->ms_windows > 0 ? (long)cmd->ms_windows : (long)win.size());
         std::vector<int32_t> wpos;
         std::vector<uint64_t> wtypes;
         for (auto &x : win) {
@@ -626,9 +676,21 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         }
     }
     if (needed) *needed = text.size() + 1;
-    if (text.size() + 1 > cap) return fail(c, PBG_E_RANGE, "output buffer too small");
+    if (text.size() + 1 > cap) {
+        c->text.swap(text);   // kept for pbg_take_text
+        return fail(c, PBG_E_RANGE, "output buffer too small");
+    }
     std::memcpy(out, text.c_str(), text.size() + 1);
     return (long)text.size();
+}
+
+long pbg_take_text(pbg_ctx *c, char *out, size_t cap) {
+    if (!c || (!out && cap)) return fail(c, PBG_E_ARG, "null argument");
+    if (c->text.size() + 1 > cap) return fail(c, PBG_E_RANGE, "output buffer too small");
+    std::memcpy(out, c->text.c_str(), c->text.size() + 1);
+    const long len = (long)c->text.size();
+    std::string().swap(c->text);
+    return len;
 }
 
 long pbg_format(const pbg_ctx *c, const pbg_cmd *cmd, const pbg_window_out *ho, uint32_t n_win, const int32_t *wbeg,

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/popbam_feed.h"
+#include "pbg_key.h"
 
 namespace {
 
@@ -655,6 +656,145 @@ int pbf_pileup_mt(const char *path, int n_threads, int32_t chunk, int tid, int32
         pbf_batch_free(&p);
     }
     out->block_off[((size_t)L + 63) / 64] = roff;
+    return PBF_OK;
+}
+
+void pbf_keys_free(pbf_keys *o) {
+    if (!o) return;
+    free(o->ref);
+    free(o->k);
+    free(o->rmsq);
+    free(o->block_off);
+    free(o->keys);
+    memset(o, 0, sizeof(*o));
+}
+
+int pbf_pack(const pbf_batch *raw, int ns, const pbf_filter *f, pbf_keys *out) {
+    if (!raw || !f || !out || ns < 1 || (f->k_bytes != 1 && f->k_bytes != 2)) return fail(PBF_E_ARG, "bad argument");
+    memset(out, 0, sizeof(*out));
+    const uint32_t L = raw->n_sites;
+    const size_t nt = (size_t)L * ns;
+    const int kb = f->k_bytes;
+    out->n_sites = L;
+    out->pos0 = raw->pos0;
+    out->ref = (uint8_t *)malloc(std::max<size_t>(L, 1));
+    out->k = calloc(std::max<size_t>(nt, 1), kb);
+    out->rmsq = (uint32_t *)calloc(std::max<size_t>(nt, 1), sizeof(uint32_t));
+    out->block_off = (uint64_t *)calloc(L / 64 + 2, sizeof(uint64_t));
+    out->keys = (uint16_t *)aligned_alloc(16, (std::max<uint64_t>(raw->n_reads, 1) * 2 + 15) & ~(size_t)15);
+    if (!out->ref || !out->k || !out->rmsq || !out->block_off || !out->keys) {
+        pbf_keys_free(out);
+        return fail(PBF_E_IO, "out of host memory");
+    }
+    if (L) memcpy(out->ref, raw->ref, L);
+    const uint32_t minb = (uint32_t)(f->min_baseQ & 0xff), minm = (uint32_t)(f->min_mapQ & 0xff);
+    const bool ill = f->illumina != 0;
+    uint64_t r = 0, nk = 0;
+    for (size_t t = 0; t < nt; ++t) {
+        if (t % ((size_t)64 * ns) == 0) out->block_off[t / ((size_t)64 * ns)] = nk;
+        const uint32_t d = raw->depth[t];
+        uint32_t kk = 0, rq = 0;
+        for (uint32_t j = 0; j < d; ++j, ++r) {
+            const uint32_t w = raw->reads[r];
+            const uint32_t key = pbg::read_to_key(w, minb, minm, ill);
+            if (!key) continue;
+            out->keys[nk++] = (uint16_t)key;
+            const uint32_t mq = (w >> 8) & 0xffu;
+            rq += mq * mq;   // rmsq += SQ(core.qual) (popbam.cpp:287)
+            ++kk;
+        }
+        if (kb == 1) {
+            if (kk > 255) {
+                pbf_keys_free(out);
+                return fail(PBF_E_ARG, "more than 255 keys per sample need k_bytes = 2");
+            }
+            ((uint8_t *)out->k)[t] = (uint8_t)kk;
+        } else {
+            ((uint16_t *)out->k)[t] = (uint16_t)kk;
+        }
+        out->rmsq[t] = rq;
+    }
+    if (r != raw->n_reads) {
+        pbf_keys_free(out);
+        return fail(PBF_E_ARG, "depth[] does not add up to n_reads");
+    }
+    out->block_off[(L + 63) / 64] = nk;
+    out->n_keys = nk;
+    return PBF_OK;
+}
+
+int pbf_pileup_keys_mt(const char *path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
+                       const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
+                       int32_t fallback, int ns, int max_depth, const pbf_filter *f, pbf_keys *out) {
+    if (!path || !out || !refseq || !f || ns < 1 || end < beg || n_threads < 1) return fail(PBF_E_ARG, "bad argument");
+    memset(out, 0, sizeof(*out));
+    const int64_t L = (int64_t)end - beg;
+    if (chunk <= 0) chunk = 1 << 20;
+    chunk = (chunk + 63) / 64 * 64;   // chunk borders on 64-position blocks: block_off concatenates
+    const int64_t nchunk = std::max<int64_t>(1, (L + chunk - 1) / chunk);
+    std::vector<pbf_keys> parts((size_t)nchunk);
+    std::vector<int> rc((size_t)nchunk, PBF_OK);
+    std::vector<std::string> msg((size_t)nchunk);
+    for (auto &p : parts) memset(&p, 0, sizeof(p));
+    const int nt = (int)std::min<int64_t>(n_threads, nchunk);
+    auto worker = [&](int w) {
+        pbf_bam *b = nullptr;
+        int r = pbf_open(&b, path);
+        for (int64_t c = w; c < nchunk; c += nt) {
+            if (r == PBF_OK) {
+                const int32_t cb = (int32_t)(beg + c * chunk), ce = (int32_t)std::min<int64_t>(end, beg + (c + 1) * chunk);
+                pbf_batch raw;
+                r = pbf_pileup(b, tid, cb, ce, refseq, rg_ids, rg_sample, n_rg, fallback, ns, max_depth, &raw);
+                if (r == PBF_OK) {
+                    r = pbf_pack(&raw, ns, f, &parts[c]);
+                    pbf_batch_free(&raw);
+                }
+            }
+            rc[c] = r;
+            if (r != PBF_OK) msg[c] = g_err;
+        }
+        if (b) pbf_close(b);
+    };
+    std::vector<std::thread> th;
+    for (int w = 1; w < nt; ++w) th.emplace_back(worker, w);
+    worker(0);
+    for (auto &t : th) t.join();
+    for (int64_t c = 0; c < nchunk; ++c)
+        if (rc[c] != PBF_OK) {
+            for (auto &p : parts) pbf_keys_free(&p);
+            return fail(rc[c], msg[c]);
+        }
+    uint64_t n_keys = 0;
+    for (auto &p : parts) n_keys += p.n_keys;
+    const int kb = f->k_bytes;
+    out->n_sites = (uint32_t)L;
+    out->pos0 = beg;
+    out->n_keys = n_keys;
+    out->ref = (uint8_t *)malloc(std::max<size_t>((size_t)L, 1));
+    out->k = malloc(std::max<size_t>((size_t)L * ns, 1) * kb);
+    out->rmsq = (uint32_t *)malloc(std::max<size_t>((size_t)L * ns, 1) * sizeof(uint32_t));
+    out->block_off = (uint64_t *)calloc((size_t)L / 64 + 2, sizeof(uint64_t));
+    out->keys = (uint16_t *)aligned_alloc(16, (std::max<uint64_t>(n_keys, 1) * 2 + 15) & ~(size_t)15);
+    if (!out->ref || !out->k || !out->rmsq || !out->block_off || !out->keys) {
+        for (auto &p : parts) pbf_keys_free(&p);
+        pbf_keys_free(out);
+        return fail(PBF_E_IO, "out of host memory");
+    }
+    size_t site = 0;
+    uint64_t koff = 0;
+    for (auto &p : parts) {   // each part is released as soon as it is copied
+        if (p.n_sites) {
+            memcpy(out->ref + site, p.ref, p.n_sites);
+            memcpy((char *)out->k + site * ns * kb, p.k, (size_t)p.n_sites * ns * kb);
+            memcpy(out->rmsq + site * ns, p.rmsq, (size_t)p.n_sites * ns * sizeof(uint32_t));
+            for (uint32_t bk = 0; bk * 64 < p.n_sites; ++bk) out->block_off[site / 64 + bk] = koff + p.block_off[bk];
+        }
+        if (p.n_keys) memcpy(out->keys + koff, p.keys, p.n_keys * sizeof(uint16_t));
+        site += p.n_sites;
+        koff += p.n_keys;
+        pbf_keys_free(&p);
+    }
+    out->block_off[((size_t)L + 63) / 64] = koff;
     return PBF_OK;
 }
 

@@ -4,6 +4,8 @@
 #include <stdint.h>
 
 #include "../../include/popbam_gpu.h"
+#define PBG_HD __host__ __device__
+#include "pbg_key.h"
 
 namespace pbg {
 
@@ -17,6 +19,8 @@ struct DevParams {
     int32_t pop_n[PBG_MAX_POPS];
     int32_t min_depth, max_depth, min_rmsQ, min_snpQ, min_mapQ, min_baseQ;
     uint32_t flag;
+    int32_t k16;          // k[] is u16 (max_depth > 255), else u8
+    int32_t sfs_stride;   // largest population + 1 (pbg_window_out.sfs_bins row)
 };
 
 // Host-built tables resident in HBM for the lifetime of a context.
@@ -46,15 +50,16 @@ __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
     return z ^ (z >> 31);
 }
 
-// Synthetic pileup (benchmark workload): site hash keyed on (seed, pos).
+// Synthetic pileup (benchmark workload): site hash keyed on (seed, contig,
+// pos); contig 0 hashes the position alone.
 struct SynthSite {
     uint64_t h;
     int ref_idx, alt, snp;
     uint32_t f16;
 };
-__host__ __device__ inline SynthSite synth_site(uint64_t seed, uint64_t pos) {
+__host__ __device__ inline SynthSite synth_site(uint64_t seed, int contig, uint64_t pos) {
     SynthSite s;
-    s.h = splitmix64(seed ^ splitmix64(pos));
+    s.h = splitmix64(seed ^ splitmix64(pos ^ ((uint64_t)(uint32_t)contig << 40)));
     s.ref_idx = (int)(s.h & 3);
     s.snp = ((s.h >> 2) & 0x3FF) < 12;          // theta ~ 0.012
     s.alt = (s.ref_idx + 1 + (int)((s.h >> 12) % 3)) & 3;
@@ -114,8 +119,8 @@ struct StatsArgs {
 // position for a final fold.  A task that does not fit in the queue is computed in place.
 struct DeepTask {
     uint32_t site;
-    uint32_t sd;        // sample | depth << 8
-    uint64_t off;       // index in reads[] of the task's first read
+    uint32_t sd;        // sample | k << 8
+    uint64_t off;       // index in keys[] of the task's first key
 };
 struct DeepBufs {
     uint32_t *sites;    // [n_sites] positions with a queued task
@@ -128,25 +133,36 @@ struct DeepBufs {
     // reads from the start, deeper ones from the end; blk_cnt[b] = shallow | deep << 16
     uint32_t *blk_cnt;
     uint32_t blk_cap;
-    uint4 *raw;         // [nblk*blk_cap*4]: the reads of front (<= 16 reads) entries, copied by the
-                        // scan kernel from its LDS staging so the queue kernel loads them coalesced
+    uint4 *raw;         // [nblk*blk_cap*2]: the 16 keys of front (<= 16 keys) entries (32 B, the
+                        // entry header in key bits 11-15), copied by the scan kernel from its LDS
+                        // staging so the queue kernel loads them coalesced
 };
 #ifndef PBG_QGROUP
 #define PBG_QGROUP 16
 #endif
 constexpr int kQueueGroup = PBG_QGROUP;   // blocks per wave in the queue kernels
 
+// A device pileup batch as the kernels see it (pbg_pileup with the k width resolved).
+struct Batch {
+    uint32_t n_sites;
+    const uint8_t *ref;
+    const void *k;                 // u8 or u16 (DevParams::k16)
+    const uint32_t *rmsq;
+    const uint64_t *block_off;
+    const uint16_t *keys;
+};
+
 // kernel launchers (defined in call_kernel.hip / stats_kernel.hip)
-hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, uint32_t n_sites,
-                             const uint8_t *ref, const uint16_t *depth, const uint64_t *block_off,
-                             const uint32_t *reads, uint32_t cap, void *rows, uint64_t *cb, int *err,
-                             const struct DeepBufs &D, hipStream_t stream, hipEvent_t ev0 = nullptr,
-                             hipEvent_t ev1 = nullptr);
+hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, const Batch &B, uint32_t cap,
+                             void *rows, uint64_t *cb, int *err, const struct DeepBufs &D, hipStream_t stream,
+                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 size_t call_sites_lds_bytes(int n, uint32_t cap);
-hipError_t launch_synth_depth(uint64_t seed, int mean_depth, int n, uint32_t n_sites, uint8_t *ref,
-                              uint16_t *depth, uint64_t *block_tot, hipStream_t stream);
-hipError_t launch_synth_reads(uint64_t seed, int mean_depth, int n, uint32_t n_sites, const uint16_t *depth,
-                              const uint64_t *block_off, uint32_t *reads, hipStream_t stream);
+// synthetic batch: k / rmsq / ref + per-block key totals, then an exclusive scan of the totals
+// into block_off (scratch: one u64 per 1024 blocks), then the keys
+hipError_t launch_synth(const DevParams &P, uint64_t seed, int contig, int mean_depth, int64_t pos0, uint32_t n_sites,
+                        uint8_t *ref, void *k, uint32_t *rmsq, uint64_t *block_off, uint16_t *keys,
+                        uint64_t keys_cap, uint64_t *scratch, int *err, hipStream_t stream);
+size_t synth_scratch_words(uint32_t n_sites);
 hipError_t launch_window_stats(int row_bytes, const DevParams &P, const DevTables &T, const void *rows,
                                uint32_t n_rows, uint32_t n_win, const StatsArgs &A, hipStream_t stream);
 

@@ -1,9 +1,10 @@
 """One `popbam <cmd>` invocation on the GPU (host-side mirror of main_<cmd>).
 
 `run_command` takes what the reference derives before its window loop -- parsed options
-(popbam_amd.options), the @RG sample model, the region -- plus the dense pileup batch the
-host side of the pileup callback produced, and returns the reference's stdout.  All
-compute runs in libpopbam_gpu.so (pbg_run); there is no CPU path.
+(popbam_amd.options), the @RG sample model, the region -- plus the key batch the host side
+of the pileup callback produced (popbam_amd.feed: pileup, per-sample partition and call_base's
+per-read loop), and returns the reference's stdout.  All compute runs in libpopbam_gpu.so
+(pbg_run); there is no CPU path.
 """
 from __future__ import annotations
 
@@ -12,6 +13,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
+from . import feed
 from . import options as opt
 
 
@@ -30,9 +32,14 @@ def make_params(o: opt.Options, sm: opt.SampleModel) -> _lib.PbgParams:
     return p
 
 
+def make_filter(o: opt.Options):
+    """call_base's per-read filters for the host side of the callback (popbam.cpp:266-281)."""
+    return feed.make_filter(o.min_baseQ, o.min_mapQ, o.flag, o.max_depth)
+
+
 class _Cmd:
     def __init__(self, o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, end: int,
-                 refid: str = ""):
+                 refid: str = "", ms_windows: int = 0):
         c = _lib.PbgCmd()
         c.cmd = opt.CMD_IDS[o.cmd]
         c.output, c.min_sites, c.min_snps, c.min_freq = o.output, o.min_sites, o.min_snps, o.min_freq
@@ -54,33 +61,37 @@ class _Cmd:
         c.pop_names = C.cast(self._pn, C.POINTER(C.c_char_p))
         self._refid = refid.encode()
         c.refid = self._refid
+        c.ms_windows = ms_windows
         self.c = c
 
 
 def run_command(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg: int, end: int, batch: dict,
-                pos0: int = 0, device: int = 0, ctx: _lib.Context | None = None, refid: str = "") -> str:
-    """batch: {'ref': u8[n_sites], 'depth': u16[n_sites, n], 'reads': u32[...]} (host)."""
+                pos0: int = 0, device: int = 0, ctx: _lib.Context | None = None, refid: str = "",
+                ms_windows: int = 0) -> str:
+    """batch: the key batch {'ref': u8[n_sites], 'k': u8/u16[n_sites, n], 'rmsq': u32[n_sites, n],
+    'keys': u16[...]} (host; popbam_amd.feed)."""
     own = ctx is None
     if own:
         ctx = _lib.Context(make_params(o, sm), device)
     try:
+        kt = np.uint8 if ctx.k_bytes == 1 else np.uint16
         ref = np.ascontiguousarray(batch["ref"], dtype=np.uint8)
-        dep = np.ascontiguousarray(batch["depth"], dtype=np.uint16)
-        rd = np.ascontiguousarray(batch["reads"], dtype=np.uint32)
-        if rd.size == 0:
-            rd = np.zeros(1, np.uint32)
-        pl = _lib.PbgPileup(len(ref), pos0, ref.ctypes.data, dep.ctypes.data, None, rd.ctypes.data)
-        cmd = _Cmd(o, sm, chr_name, beg, end, refid)
+        k = np.ascontiguousarray(batch["k"], dtype=kt)
+        rq = np.ascontiguousarray(batch["rmsq"], dtype=np.uint32)
+        keys = np.ascontiguousarray(batch["keys"], dtype=np.uint16)
+        if keys.size == 0:
+            keys = np.zeros(8, np.uint16)
+        pl = _lib.PbgPileup(len(ref), pos0, ref.ctypes.data, k.ctypes.data, rq.ctypes.data, None, keys.ctypes.data)
+        cmd = _Cmd(o, sm, chr_name, beg, end, refid, ms_windows)
         need = C.c_size_t(0)
         cap = 1 << 20
-        while True:
-            buf = C.create_string_buffer(cap)
-            r = ctx.lib.pbg_run(ctx.h, C.byref(cmd.c), C.byref(pl), buf, cap, C.byref(need))
-            if r == _lib.PBG_E_RANGE and need.value > cap:
-                cap = need.value
-                continue
-            ctx.check(r, "pbg_run")
-            return buf.value.decode()
+        buf = C.create_string_buffer(cap)
+        r = ctx.lib.pbg_run(ctx.h, C.byref(cmd.c), C.byref(pl), buf, cap, C.byref(need))
+        if r == _lib.PBG_E_RANGE and need.value > cap:
+            buf = C.create_string_buffer(need.value)   # the text is kept by the context
+            r = ctx.lib.pbg_take_text(ctx.h, buf, need.value)
+        ctx.check(r, "pbg_run")
+        return buf.value.decode()
     finally:
         if own:
             ctx.close()

@@ -14,7 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libpopbam_feed.so")
 
 EXPORTS = ["pbf_last_error", "pbf_open", "pbf_close", "pbf_header_text", "pbf_n_refs", "pbf_ref_name",
-           "pbf_ref_len", "pbf_has_index", "pbf_pileup", "pbf_pileup_mt", "pbf_batch_free", "pbf_fasta_fetch", "pbf_free"]
+           "pbf_ref_len", "pbf_has_index", "pbf_pileup", "pbf_pileup_mt", "pbf_batch_free", "pbf_fasta_fetch", "pbf_free",
+           "pbf_pack", "pbf_keys_free", "pbf_pileup_keys_mt"]
 
 PBF_E_RG = -4
 
@@ -23,6 +24,21 @@ class PbfBatch(C.Structure):
     _fields_ = [("n_sites", C.c_uint32), ("pos0", C.c_int32), ("ref", C.POINTER(C.c_uint8)),
                 ("depth", C.POINTER(C.c_uint16)), ("block_off", C.POINTER(C.c_uint64)),
                 ("reads", C.POINTER(C.c_uint32)), ("n_reads", C.c_uint64)]
+
+
+class PbfKeys(C.Structure):
+    _fields_ = [("n_sites", C.c_uint32), ("pos0", C.c_int32), ("ref", C.POINTER(C.c_uint8)), ("k", C.c_void_p),
+                ("rmsq", C.POINTER(C.c_uint32)), ("block_off", C.POINTER(C.c_uint64)),
+                ("keys", C.POINTER(C.c_uint16)), ("n_keys", C.c_uint64)]
+
+
+class PbfFilter(C.Structure):
+    _fields_ = [("min_baseQ", C.c_int32), ("min_mapQ", C.c_int32), ("illumina", C.c_int32), ("k_bytes", C.c_int32)]
+
+
+def make_filter(min_baseQ: int, min_mapQ: int, flag: int, max_depth: int) -> PbfFilter:
+    """call_base's per-read filters (popbam.cpp:266-281) and the k width for max_depth."""
+    return PbfFilter(min_baseQ & 0xFF, min_mapQ & 0xFF, 1 if flag & 0x02 else 0, 1 if max_depth <= 255 else 2)
 
 
 class FeedError(RuntimeError):
@@ -60,6 +76,12 @@ def load():
                                   P(C.c_char_p), P(C.c_int32), C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfBatch)]
     lib.pbf_batch_free.argtypes = [P(PbfBatch)]
     lib.pbf_batch_free.restype = None
+    lib.pbf_pack.argtypes = [P(PbfBatch), C.c_int, P(PbfFilter), P(PbfKeys)]
+    lib.pbf_keys_free.argtypes = [P(PbfKeys)]
+    lib.pbf_keys_free.restype = None
+    lib.pbf_pileup_keys_mt.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int, C.c_int32, C.c_int32, C.c_char_p,
+                                       P(C.c_char_p), P(C.c_int32), C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfFilter),
+                                       P(PbfKeys)]
     lib.pbf_fasta_fetch.argtypes = [C.c_char_p, C.c_char_p, P(C.c_void_p), P(C.c_int64)]
     lib.pbf_free.argtypes = [vp]
     lib.pbf_free.restype = None
@@ -82,6 +104,42 @@ def fasta_fetch(path: str, name: str) -> bytes:
         return C.string_at(p, n.value)
     finally:
         lib.pbf_free(p)
+
+
+def _take_keys(lib, out: PbfKeys, n_samples: int, kb: int) -> dict:
+    try:
+        L = out.n_sites
+        ref = np.ctypeslib.as_array(out.ref, (max(L, 1),))[:L].copy()
+        kt = C.c_uint8 if kb == 1 else C.c_uint16
+        k = np.ctypeslib.as_array(C.cast(out.k, C.POINTER(kt)), (max(L * n_samples, 1),))[:L * n_samples].copy()
+        rmsq = np.ctypeslib.as_array(out.rmsq, (max(L * n_samples, 1),))[:L * n_samples].copy()
+        keys = np.ctypeslib.as_array(out.keys, (max(out.n_keys, 1),))[:out.n_keys].copy()
+        boff = np.ctypeslib.as_array(out.block_off, ((L + 63) // 64 + 1,)).copy()
+    finally:
+        lib.pbf_keys_free(C.byref(out))
+    return {"ref": ref, "k": k.reshape(L, n_samples), "rmsq": rmsq.reshape(L, n_samples), "keys": keys,
+            "block_off": boff, "pos0": out.pos0}
+
+
+def pack(batch: dict, n_samples: int, flt: PbfFilter) -> dict:
+    """pbf_pack: a raw batch ({'ref', 'depth', 'reads'}: the callback's per-sample partition)
+    -> the key batch pbg_call_sites / pbg_run take (call_base's per-read loop applied)."""
+    lib = load()
+    ref = np.ascontiguousarray(batch["ref"], dtype=np.uint8)
+    dep = np.ascontiguousarray(batch["depth"], dtype=np.uint16).reshape(-1)
+    rd = np.ascontiguousarray(batch["reads"], dtype=np.uint32)
+    if rd.size == 0:
+        rd = np.zeros(1, np.uint32)
+    raw = PbfBatch()
+    raw.n_sites, raw.pos0 = len(ref), int(batch.get("pos0", 0))
+    raw.ref = ref.ctypes.data_as(C.POINTER(C.c_uint8))
+    raw.depth = dep.ctypes.data_as(C.POINTER(C.c_uint16))
+    raw.block_off = None
+    raw.reads = rd.ctypes.data_as(C.POINTER(C.c_uint32))
+    raw.n_reads = int(np.asarray(batch["depth"], dtype=np.int64).sum())
+    out = PbfKeys()
+    _check(lib, lib.pbf_pack(C.byref(raw), n_samples, C.byref(flt), C.byref(out)))
+    return _take_keys(lib, out, n_samples, flt.k_bytes)
 
 
 class Bam:
@@ -129,6 +187,21 @@ class Bam:
         finally:
             self.lib.pbf_batch_free(C.byref(out))
         return {"ref": ref, "depth": depth.reshape(L, n_samples), "reads": reads, "block_off": boff, "pos0": beg}
+
+    def pileup_keys(self, tid: int, beg: int, end: int, refseq: bytes, rg2s: dict, n_samples: int, max_depth: int,
+                    flt: PbfFilter, fallback_sample: int = -1, threads: int = 1, chunk: int = 1 << 20) -> dict:
+        """Key batch of [beg, end) (pbf_pileup_keys_mt): pileup + partition + call_base's
+        per-read loop, pieces walked and packed by `threads` threads."""
+        ids = list(rg2s)
+        rg = (C.c_char_p * max(1, len(ids)))(*[i.encode() for i in ids])
+        sm = (C.c_int32 * max(1, len(ids)))(*[rg2s[i] for i in ids])
+        if len(refseq) < end:
+            raise FeedError(-3, "reference sequence shorter than the region")
+        out = PbfKeys()
+        _check(self.lib, self.lib.pbf_pileup_keys_mt(self.path.encode(), max(1, threads), chunk, tid, beg, end, refseq,
+                                                     rg, sm, len(ids), fallback_sample, n_samples, max_depth,
+                                                     C.byref(flt), C.byref(out)))
+        return _take_keys(self.lib, out, n_samples, flt.k_bytes)
 
     def close(self):
         if self.h:

@@ -54,10 +54,16 @@ def positions_needed(beg: int, end: int, win_size: int, windowed: bool) -> tuple
 
 def slice_batch(batch: dict, pos0: int, lo: int, hi: int) -> dict:
     """The part of a host pileup batch (positions [pos0, pos0 + len(ref))) that covers
-    [lo, hi): ref/depth rows and the matching run of reads."""
+    [lo, hi): per-position rows and the matching run of reads (raw batch: 'depth' / 'reads')
+    or keys (key batch: 'k' / 'rmsq' / 'keys')."""
     n_sites = len(batch["ref"])
     a = min(max(lo - pos0, 0), n_sites)
     b = min(max(hi - pos0, a), n_sites)
+    if "keys" in batch:
+        k = np.asarray(batch["k"])
+        cum = np.concatenate([[0], np.cumsum(k.sum(axis=1, dtype=np.int64))])
+        return {"ref": np.asarray(batch["ref"])[a:b], "k": k[a:b], "rmsq": np.asarray(batch["rmsq"])[a:b],
+                "keys": np.asarray(batch["keys"])[cum[a]:cum[b]], "pos0": pos0 + a}
     dep = np.asarray(batch["depth"])
     cum = np.concatenate([[0], np.cumsum(dep.sum(axis=1, dtype=np.int64))])
     return {"ref": np.asarray(batch["ref"])[a:b], "depth": dep[a:b],

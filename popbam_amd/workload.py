@@ -43,44 +43,65 @@ def default_params(n_samples: int, n_pops: int = 2, **kw) -> _lib.PbgParams:
 
 
 class SynthPileup:
+    """Synthetic key batch in HBM (pbg_synth_pileup): positions [pos0, pos0 + n_sites) of
+    `contig`, with the context's filters applied.  keys[] is sized exactly (one host sync)
+    unless `keys_cap` is given (then no sync: pipelined producers pass the upper bound)."""
+
     def __init__(self, ctx: _lib.Context, n_sites: int, mean_depth: int = 10, seed: int = 0xC0FFEE02,
-                 device: str = "cuda"):
+                 device: str = "cuda", contig: int = 0, pos0: int = 0, keys_cap: int | None = None,
+                 stream: torch.cuda.Stream | None = None):
         self.ctx, self.n_sites, self.mean_depth, self.seed = ctx, n_sites, mean_depth, seed
+        self.contig, self.pos0 = contig, pos0
         n = ctx.params.n_samples
         nblk = (n_sites + SITE_BLOCK - 1) // SITE_BLOCK
-        self.ref = torch.empty(n_sites, dtype=torch.uint8, device=device)
-        self.depth = torch.empty(n_sites * n, dtype=torch.int16, device=device)
+        self.spec = _lib.PbgSynthSpec(seed, contig, mean_depth, pos0, n_sites)
+        self.ref = torch.empty(max(1, n_sites), dtype=torch.uint8, device=device)
+        self.k = torch.empty(max(1, n_sites * n), dtype=torch.uint8 if ctx.k_bytes == 1 else torch.int16,
+                             device=device)
+        self.rmsq = torch.empty(max(1, n_sites * n), dtype=torch.int32, device=device)
         self.block_off = torch.zeros(nblk + 1, dtype=torch.int64, device=device)
-        nr = C.c_uint64(0)
-        s = stream_handle()
-        ctx.check(ctx.lib.pbg_synth_depth(ctx.h, seed, mean_depth, n_sites, _ptr(self.ref), _ptr(self.depth),
-                                          _ptr(self.block_off), C.byref(nr), s), "pbg_synth_depth")
-        self.n_reads = nr.value
-        self.reads = torch.empty(max(1, self.n_reads), dtype=torch.int32, device=device)
-        ctx.check(ctx.lib.pbg_synth_reads(ctx.h, seed, mean_depth, n_sites, _ptr(self.depth), _ptr(self.block_off),
-                                          _ptr(self.reads), s), "pbg_synth_reads")
-        torch.cuda.synchronize()
+        self.max_keys = int(ctx.lib.pbg_synth_max_keys(ctx.h, C.byref(self.spec)))
+        if keys_cap is None:   # exact size: a counting pass (keys = NULL), then the batch
+            nk = C.c_uint64(0)
+            ctx.check(ctx.lib.pbg_synth_pileup(ctx.h, C.byref(self.spec), _ptr(self.ref), _ptr(self.k),
+                                               _ptr(self.rmsq), _ptr(self.block_off), None, 0, C.byref(nk),
+                                               stream_handle(stream)), "pbg_synth_pileup")
+            keys_cap = nk.value
+        self.keys_cap = keys_cap
+        self.keys = torch.empty(max(8, keys_cap), dtype=torch.int16, device=device)
+        self.n_keys = None
+        self.generate(stream, sync=True)
+
+    def generate(self, stream=None, sync: bool = True):
+        """(Re)generate the batch on `stream` (asynchronous unless sync)."""
+        s = stream_handle(stream)
+        nk = C.c_uint64(0)
+        self.ctx.check(self.ctx.lib.pbg_synth_pileup(self.ctx.h, C.byref(self.spec), _ptr(self.ref), _ptr(self.k),
+                                                     _ptr(self.rmsq), _ptr(self.block_off), _ptr(self.keys),
+                                                     self.keys_cap, C.byref(nk) if sync else None, s),
+                       "pbg_synth_pileup")
+        if sync:
+            self.n_keys = nk.value
 
     def pileup(self) -> _lib.PbgPileup:
-        return _lib.PbgPileup(self.n_sites, 0, _ptr(self.ref), _ptr(self.depth), _ptr(self.block_off),
-                              _ptr(self.reads))
+        return _lib.PbgPileup(self.n_sites, self.pos0, _ptr(self.ref), _ptr(self.k), _ptr(self.rmsq),
+                              _ptr(self.block_off), _ptr(self.keys))
 
-    def bytes_read_by_call(self) -> int:
-        """Algorithmic HBM bytes of the call stage: every read record (4 B), the depth matrix
-        (2 B per site x sample), the reference byte, the block offsets, and the packed rows
-        it writes."""
+    def survey_bytes(self) -> int:
+        """SURVEY 8(d) algorithmic bytes of the call stage for this batch: per (position,
+        sample) 2k + 5 (u16 keys, u8 k, u32 sum mapQ^2), per position 1 (reference byte) +
+        row_bytes written."""
+        n = self.ctx.params.n_samples
+        return 2 * self.n_keys + 5 * self.n_sites * n + self.n_sites * (1 + self.ctx.row_bytes)
+
+    def layout_bytes_scan(self) -> int:
+        """Bytes one call_scan_kernel launch must move in this layout: the keys, k (k_bytes),
+        rmsq, reference bytes and block offsets read, one info byte per (position, sample)
+        written (queue entries not counted)."""
         n = self.ctx.params.n_samples
         nblk = (self.n_sites + SITE_BLOCK - 1) // SITE_BLOCK
-        return 4 * self.n_reads + 2 * self.n_sites * n + self.n_sites + 8 * (nblk + 1) + \
-            self.ctx.row_bytes * self.n_sites
-
-    def bytes_scan_kernel(self) -> int:
-        """Algorithmic HBM bytes of one call_scan_kernel launch (the dominant kernel of the
-        rows-only call): every read record (4 B), the depths (2 B per site x sample), the
-        reference byte, the block offsets, and one info byte written per (site, sample)."""
-        n = self.ctx.params.n_samples
-        nblk = (self.n_sites + SITE_BLOCK - 1) // SITE_BLOCK
-        return 4 * self.n_reads + 2 * self.n_sites * n + self.n_sites + 8 * (nblk + 1) + self.n_sites * n
+        return (2 * self.n_keys + (self.ctx.k_bytes + 4 + 1) * self.n_sites * n + self.n_sites +
+                8 * (nblk + 1))
 
 
 def reference_windows(beg: int, end: int, win_size: int):
@@ -92,8 +113,9 @@ def reference_windows(beg: int, end: int, win_size: int):
 class WindowOutputs:
     """Device arrays for pbg_window_out (all statistics)."""
 
-    def __init__(self, n_win: int, n: int, np_: int, device: str = "cuda"):
+    def __init__(self, n_win: int, n: int, np_: int, device: str = "cuda", sfs_stride: int | None = None):
         npairs = max(1, np_ * (np_ - 1))
+        sfs_stride = sfs_stride or n + 1
         f64 = dict(dtype=torch.float64, device=device)
         i32 = dict(dtype=torch.int32, device=device)
         self.t = {
@@ -107,6 +129,8 @@ class WindowOutputs:
             "hap_val": torch.zeros(n_win * np_, **f64), "hap_dxy": torch.zeros(n_win * npairs, **f64),
             "hap_min": torch.zeros(n_win * npairs, **i32),
             "tree_diff": torch.zeros(n_win * (n + 1) * (n + 1), **i32),
+            "sfs_bins": torch.zeros(n_win * np_ * sfs_stride, **i32), "seg_pop": torch.zeros(n_win * np_, **i32),
+            "theta_w": torch.zeros(n_win * np_, **f64),
         }
 
     def struct(self, fields) -> _lib.PbgWindowOut:
@@ -127,12 +151,12 @@ class HotPath:
         self.wins = w.to(device)
         self.n_win = len(windows)
         p = ctx.params
-        self.out = WindowOutputs(self.n_win, p.n_samples, p.n_pops, device)
+        self.out = WindowOutputs(self.n_win, p.n_samples, p.n_pops, device, ctx.sfs_stride)
         fields = ["num_sites", "segsites"]
         if stats & _lib.PBG_S_NUCDIV:
             fields += ["pi", "dxy"]
         if stats & _lib.PBG_S_SFS:
-            fields += ["td", "fwh"]
+            fields += ["td", "fwh", "sfs_bins", "seg_pop", "theta_w"]
         if stats & (_lib.PBG_S_ZNS | _lib.PBG_S_OMEGA | _lib.PBG_S_WALL):
             fields += ["ld_snps", "ld_val", "ld_q"]
         if stats & _lib.PBG_S_DIV_IND:

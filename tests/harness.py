@@ -54,9 +54,9 @@ def oracle():
         lib.orc_windows_from_sites.restype = C.c_long
         lib.orc_windows_from_sites.argtypes = [P(OrcParams), P(OrcCmd), C.c_void_p, C.c_void_p, C.c_uint32,
                                                C.c_void_p, C.c_void_p, C.c_char_p, C.c_size_t]
-        lib.orc_synth_site.restype = None
-        lib.orc_synth_site.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
-                                       C.c_void_p, C.c_void_p]
+        lib.orc_synth_batch.restype = C.c_uint64
+        lib.orc_synth_batch.argtypes = [C.c_uint64, C.c_int32, C.c_uint64, C.c_uint32, C.c_int32, C.c_int32,
+                                        C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
         for nm in ("orc_fk", "orc_beta", "orc_lhet"):
             getattr(lib, nm).restype = P(C.c_double)
         _orc = lib
@@ -82,6 +82,15 @@ class Setup:
         self.chr = names[self.tid]
         self.refid = opt.get_refid(self.case["header"]) if args[0] == "tree" else ""
         self.batch = fixtures.case_batch(case_name, o.max_depth)
+        self._kbatch = None
+
+    @property
+    def kbatch(self):
+        """The fixture's key batch (feed.pack of the raw batch with this command's filters)."""
+        if self._kbatch is None:
+            from popbam_amd import engine, feed
+            self._kbatch = feed.pack(self.batch, self.sm.n, engine.make_filter(self.opts))
+        return self._kbatch
 
     def orc_params(self):
         o = self.opts
@@ -179,24 +188,25 @@ def snp_oob_cells(oracle_text: str):
     return out
 
 
-def synth_batch(seed, pos_lo, pos_hi, n, mean_depth):
+def synth_batch(seed, pos_lo, pos_hi, n, mean_depth, max_depth=255, contig=0):
     """Regenerate positions [pos_lo, pos_hi) of the synthetic pileup on the CPU (oracle copy
-    of the generator) as a dense host batch."""
+    of the generator) as a raw host batch (the callback's partition, max_depth cap applied)."""
     lib = oracle()
     L = pos_hi - pos_lo
-    ref = np.zeros(L, np.uint8)
-    dep = np.zeros((L, n), np.uint16)
-    buf = np.zeros(n * 2 * mean_depth + 1, np.uint32)
-    parts = []
-    r = np.zeros(1, np.uint8)
-    nr = np.zeros(1, np.uint32)
-    for i in range(L):
-        lib.orc_synth_site(seed, pos_lo + i, n, mean_depth, r.ctypes.data, dep[i].ctypes.data, buf.ctypes.data,
-                           nr.ctypes.data)
-        ref[i] = r[0]
-        parts.append(buf[:nr[0]].copy())
-    reads = np.concatenate(parts) if parts else np.zeros(0, np.uint32)
-    return dict(ref=ref, depth=dep, reads=reads)
+    ref = np.zeros(max(L, 1), np.uint8)
+    dep = np.zeros((max(L, 1), n), np.uint16)
+    reads = np.zeros(max(1, L * n * min(2 * mean_depth, max_depth)), np.uint32)
+    nr = lib.orc_synth_batch(seed, contig, pos_lo, L, n, mean_depth, max_depth, ref.ctypes.data, dep.ctypes.data,
+                             reads.ctypes.data)
+    return dict(ref=ref[:L], depth=dep[:L], reads=reads[:nr].copy())
+
+
+def key_batch(batch, params):
+    """The key batch the host side of the callback builds from a raw batch (product code:
+    libpopbam_feed.so pbf_pack, call_base's per-read loop) -- what the GPU is given."""
+    from popbam_amd import feed
+    flt = feed.make_filter(params.min_baseQ, params.min_mapQ, params.flag, params.max_depth)
+    return feed.pack(batch, params.n_samples, flt)
 
 
 def oracle_params_from(pbg_params):

@@ -40,6 +40,7 @@ def test_no_device_no_fallback():
     p = _lib.PbgParams()
     p.n_samples, p.n_pops = 2, 1
     p.pop_mask[0], p.pop_n[0] = 3, 2
+    p.max_depth = 255
     h = C.c_void_p()
     assert lib.pbg_create(C.byref(h), 0, C.byref(p)) == _lib.PBG_E_NODEV
 

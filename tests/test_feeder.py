@@ -107,3 +107,62 @@ def test_multithreaded_pileup_equals_sequential(name):
             for k in ("ref", "depth", "reads", "block_off"):
                 assert np.array_equal(one[k], mt[k]), (name, beg, end, threads, chunk, k)
     bam.close()
+
+
+def _py_pack(batch, n, min_baseQ, min_mapQ, illumina):
+    """numpy restatement of call_base's per-read loop (popbam.cpp:252-287) for the check."""
+    r = batch["reads"].astype(np.int64)
+    raw = r & 0xFF
+    bq = np.where(raw > 31, raw - 31, 0) if illumina else raw
+    mq = (r >> 8) & 0xFF
+    nt = (r >> 16) & 0xF
+    ok = (bq >= (min_baseQ & 0xFF)) & (mq >= (min_mapQ & 0xFF)) & np.isin(nt, [1, 2, 4, 8])
+    base = np.select([nt == 1, nt == 2, nt == 4], [0, 1, 2], 3)
+    qq = np.clip(np.minimum(bq, mq), 4, 63)
+    key = (qq << 5) | (((r >> 20) & 1) << 4) | base
+    task = np.repeat(np.arange(batch["depth"].size), batch["depth"].reshape(-1).astype(np.int64))
+    k = np.bincount(task[ok], minlength=batch["depth"].size)
+    rmsq = np.bincount(task[ok], weights=(mq * mq)[ok], minlength=batch["depth"].size).astype(np.int64)
+    return k.reshape(-1, n), rmsq.reshape(-1, n), key[ok].astype(np.uint16)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_key_batches(name):
+    """pbf_pileup_keys_mt (pileup + partition + call_base's per-read loop, threaded) equals
+    pbf_pack of the restated raw batch, and pbf_pack equals a numpy restatement of the loop,
+    for the filter settings the case's commands use."""
+    c = fixtures.load_case(name)
+    bam = feed.Bam(os.path.join(c["dir"], "in.bam"))
+    seq = feed.fasta_fetch(os.path.join(c["dir"], "ref.fa"), bam.refs[0][0])
+    sm = opt.parse_header(bam.header_text, "in.bam")
+    fb = 0 if not sm.rg2sample else -1
+    seen = set()
+    for cs in c["meta"]["cases"]:
+        o = opt.parse_args(cs["args"][0], list(cs["args"][1:]) + ["in.bam", "chr1"])
+        key = (o.min_baseQ & 0xFF, o.min_mapQ & 0xFF, o.flag & 0x02, o.max_depth)
+        if key in seen:
+            continue
+        seen.add(key)
+        flt = feed.make_filter(o.min_baseQ, o.min_mapQ, o.flag, o.max_depth)
+        raw = fixtures.case_batch(name, o.max_depth)
+        packed = feed.pack(raw, sm.n, flt)
+        k, rmsq, keys = _py_pack(raw, sm.n, o.min_baseQ, o.min_mapQ, o.flag & 0x02)
+        assert np.array_equal(packed["k"], k) and np.array_equal(packed["rmsq"], rmsq)
+        assert np.array_equal(packed["keys"], keys) and np.array_equal(packed["ref"], raw["ref"])
+        cum = np.concatenate([[0], np.cumsum(k.sum(axis=1))])
+        assert np.array_equal(packed["block_off"], cum[::64] if len(k) % 64 == 0 else
+                              np.concatenate([cum[::64], cum[-1:]]))
+        for threads, chunk in [(1, 1 << 20), (4, 64), (3, 1000)]:
+            mt = bam.pileup_keys(0, 0, len(seq), seq, sm.rg2sample, sm.n, o.max_depth, flt, fb, threads=threads,
+                                 chunk=chunk)
+            for f in ("ref", "k", "rmsq", "keys", "block_off"):
+                assert np.array_equal(mt[f], packed[f]), (name, key, threads, f)
+    bam.close()
+
+
+def test_pack_rejects_wide_k_in_u8():
+    raw = fixtures.case_batch("g10_deep", 900)
+    with pytest.raises(feed.FeedError):
+        feed.pack(raw, raw["depth"].shape[1], feed.make_filter(13, 13, 0, 255))
+    wide = feed.pack(raw, raw["depth"].shape[1], feed.make_filter(13, 13, 0, 900))
+    assert wide["k"].dtype == np.uint16 and wide["k"].max() > 255

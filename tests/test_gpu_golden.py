@@ -16,7 +16,7 @@ CASES = harness.all_cases()
 def test_gpu_matches_reference(gpu_lib, name, idx):
     cs = fixtures.load_case(name)["meta"]["cases"][idx]
     st = harness.Setup(name, cs["args"], cs["region"])
-    ours = engine.run_command(st.opts, st.sm, st.chr, st.beg, st.end, st.batch, refid=st.refid)
+    ours = engine.run_command(st.opts, st.sm, st.chr, st.beg, st.end, st.kbatch, refid=st.refid)
     gold = fixtures.golden_text(name, cs["stdout"])
     oob = harness.snp_oob_cells(harness.oracle_run(st)) if cs["args"][0] == "snp" else None
     ok, diff = harness.same_output(cs["args"], gold, ours, oob)

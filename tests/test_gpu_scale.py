@@ -25,25 +25,42 @@ def _ctx(n, n_pops=2, **kw):
 SHAPES = [(12, 2), (24, 2), (24, 3), (30, 3), (48, 2), (62, 2), (64, 4)]
 
 
-def test_synthetic_generator_matches_oracle(gpu_lib):
+@pytest.mark.parametrize("n,kw,contig", [(12, {}, 0), (12, {}, 3), (24, {"flag": 0x02}, 0),
+                                          (40, {"min_baseQ": 30, "min_mapQ": 61}, 1),
+                                          (64, {"max_depth": 12, "min_depth": 8}, 0), (5, {"max_depth": 300}, 2)])
+def test_synthetic_generator_matches_oracle(gpu_lib, n, kw, contig):
+    """pbg_synth_pileup = the oracle's raw generator + the host packer (call_base's per-read
+    loop, libpopbam_feed.so), for every filter variant, k width and contig key."""
     import torch
     from popbam_amd import workload
-    ctx, params = _ctx(12)
-    syn = workload.SynthPileup(ctx, 64 * 4000, 10, SEED)
-    depth = syn.depth.cpu().numpy().view(np.uint16).reshape(-1, 12)
+    ctx, params = _ctx(n, **kw)
+    nsites = 64 * 2000 + 17
+    syn = workload.SynthPileup(ctx, nsites, 10, SEED, contig=contig, pos0=1000)
+    kt = np.uint8 if ctx.k_bytes == 1 else np.uint16
+    k = syn.k.cpu().numpy().view(kt).reshape(-1, n)
+    rq = syn.rmsq.cpu().numpy().view(np.uint32).reshape(-1, n)
     boff = syn.block_off.cpu().numpy()
-    reads = syn.reads.cpu().numpy().view(np.uint32)
+    keys = syn.keys.cpu().numpy().view(np.uint16)
     ref = syn.ref.cpu().numpy()
-    rng = np.random.default_rng(1)
-    for b in rng.choice(4000, 12, replace=False):
-        lo, hi = int(b) * 64, int(b) * 64 + 64
-        cpu = harness.synth_batch(SEED, lo, hi, 12, 10)
-        assert np.array_equal(ref[lo:hi], cpu["ref"])
-        assert np.array_equal(depth[lo:hi], cpu["depth"])
-        assert np.array_equal(reads[boff[b]:boff[b + 1]], cpu["reads"])
-    assert boff[-1] == syn.n_reads == int(depth.astype(np.int64).sum())
+    cpu = harness.key_batch(harness.synth_batch(SEED, 1000, 1000 + nsites, n, 10, params.max_depth, contig), params)
+    assert np.array_equal(ref, cpu["ref"])
+    assert np.array_equal(k, cpu["k"])
+    assert np.array_equal(rq, cpu["rmsq"])
+    assert np.array_equal(boff, cpu["block_off"])
+    assert syn.n_keys == len(cpu["keys"]) and np.array_equal(keys[:syn.n_keys], cpu["keys"])
+    # pipelined form: worst-case keys_cap, no host sync
+    syn2 = workload.SynthPileup(ctx, nsites, 10, SEED, contig=contig, pos0=1000, keys_cap=syn.max_keys)
+    assert np.array_equal(syn2.keys.cpu().numpy().view(np.uint16)[:syn.n_keys], cpu["keys"])
+    # too small a keys[]: flagged, nothing written past it
+    from popbam_amd import _lib
+    spec = syn.spec
+    small = torch.zeros(64, dtype=torch.int16, device="cuda")
+    rc = ctx.lib.pbg_synth_pileup(ctx.h, C.byref(spec), syn.ref.data_ptr(), syn.k.data_ptr(), syn.rmsq.data_ptr(),
+                                  syn.block_off.data_ptr(), small.data_ptr(), 32, None, None)
+    assert rc == 0 and ctx.lib.pbg_check(ctx.h, None) == (_lib.PBG_E_BATCH if syn.n_keys > 32 else 0)
+    assert int((small[32:] != 0).sum()) == 0
+    assert ctx.lib.pbg_check(ctx.h, None) == 0
     ctx.close()
-    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("n,kw", [
@@ -65,10 +82,10 @@ def test_call_kernel_matches_oracle(gpu_lib, n, kw):
     hp = workload.HotPath(ctx, syn, [(0, n_sites)], 0)
     cb = torch.zeros(n_sites * n, dtype=torch.int64, device="cuda")
     hp.call(cb=cb)
-    torch.cuda.synchronize()
+    ctx.sync_check()
     rows = hp.rows.cpu().numpy()
     cbh = cb.cpu().numpy().view(np.uint64).reshape(n_sites, n)
-    batch = harness.synth_batch(SEED + n, 0, n_sites, n, 10)
+    batch = harness.synth_batch(SEED + n, 0, n_sites, n, 10, params.max_depth)
     ocb, types, fq, flags = harness.oracle_call(harness.oracle_params_from(params), batch)
     bad = np.nonzero((cbh != ocb).any(axis=1))[0]
     assert bad.size == 0, f"{bad.size} positions differ, first {bad[0]}: gpu {cbh[bad[0]]} oracle {ocb[bad[0]]}"
@@ -94,9 +111,9 @@ def test_rows_only_call_matches_oracle(gpu_lib, n, kw):
     syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 7 * n)
     hp = workload.HotPath(ctx, syn, [(0, n_sites)], 0)
     hp.call()
-    torch.cuda.synchronize()
+    ctx.sync_check()
     rows = hp.rows.cpu().numpy()
-    batch = harness.synth_batch(SEED + 7 * n, 0, n_sites, n, 10)
+    batch = harness.synth_batch(SEED + 7 * n, 0, n_sites, n, 10, params.max_depth)
     _, types, _, flags = harness.oracle_call(harness.oracle_params_from(params), batch)
     expect = harness.rows_from_oracle(types, flags, ctx.row_bytes)
     bad = np.nonzero(rows != expect)[0] if rows.ndim == 1 else np.nonzero((rows != expect).any(axis=1))[0]
@@ -211,17 +228,19 @@ def test_u16_wrap_and_workspace_window(gpu_lib, n, npops):
     ctx.close()
 
 
-def _device_batch(batch, n):
+def _device_batch(kb):
+    """A host key batch -> device tensors (ref, k, rmsq, block_off, keys)."""
     import torch
-    ref = torch.from_numpy(np.ascontiguousarray(batch["ref"])).cuda()
-    dep = torch.from_numpy(np.ascontiguousarray(batch["depth"]).reshape(-1).view(np.int16)).cuda()
-    L = len(batch["ref"])
-    per_site = batch["depth"].astype(np.int64).sum(axis=1)
-    cum = np.concatenate([[0], np.cumsum(per_site)])
-    boff = torch.from_numpy(cum[::64].copy() if L % 64 == 0 else np.concatenate([cum[::64], cum[-1:]])).cuda()
-    rd = batch["reads"] if len(batch["reads"]) else np.zeros(1, np.uint32)
-    reads = torch.from_numpy(np.ascontiguousarray(rd).view(np.int32)).cuda()
-    return ref, dep, boff, reads
+    L = len(kb["ref"])
+    ref = torch.from_numpy(np.ascontiguousarray(kb["ref"])).cuda()
+    k = np.ascontiguousarray(kb["k"]).reshape(-1)
+    kd = torch.from_numpy(k if k.dtype == np.uint8 else k.view(np.int16)).cuda()
+    rq = torch.from_numpy(np.ascontiguousarray(kb["rmsq"]).reshape(-1).view(np.int32)).cuda()
+    boff = torch.from_numpy(np.ascontiguousarray(kb["block_off"]).astype(np.int64)).cuda()
+    keys = kb["keys"] if len(kb["keys"]) else np.zeros(8, np.uint16)
+    kk = torch.from_numpy(np.ascontiguousarray(keys).view(np.int16)).cuda()
+    assert len(kb["block_off"]) == (L + 63) // 64 + 1
+    return ref, kd, rq, boff, kk
 
 
 @pytest.mark.parametrize("name", ["g01_base", "g05_lowdepth", "g06_softmask", "g07_multiallelic", "g08_filters",
@@ -237,9 +256,9 @@ def test_fixture_rows_only_and_cb_paths_match_oracle(gpu_lib, name):
     params = engine.make_params(st.opts, st.sm)
     ctx = _lib.Context(params, 0)
     n = params.n_samples
-    ref, dep, boff, reads = _device_batch(st.batch, n)
+    ref, kd, rq, boff, kk = _device_batch(st.kbatch)
     L = len(st.batch["ref"])
-    pl = _lib.PbgPileup(L, 0, ref.data_ptr(), dep.data_ptr(), boff.data_ptr(), reads.data_ptr())
+    pl = _lib.PbgPileup(L, 0, ref.data_ptr(), kd.data_ptr(), rq.data_ptr(), boff.data_ptr(), kk.data_ptr())
     rb = ctx.row_bytes
     _, types, _, flags = harness.oracle_call(harness.oracle_params_from(params), st.batch)
     expect = harness.rows_from_oracle(types, flags, rb)
@@ -264,7 +283,7 @@ def test_fixture_rows_only_and_cb_paths_match_oracle(gpu_lib, name):
         cb = torch.zeros(L * n, dtype=torch.int64, device="cuda") if with_cb else None
         ctx.check(ctx.lib.pbg_call_sites(ctx.h, C.byref(pl), rows.data_ptr(), cb.data_ptr() if with_cb else None,
                                          None), "pbg_call_sites")
-        torch.cuda.synchronize()
+        ctx.sync_check()
         got = rows.cpu().numpy().reshape(L, rb)
         exp = np.ascontiguousarray(expect).view(np.uint8).reshape(L, rb)
         bad = np.nonzero((got != exp).any(axis=1))[0]

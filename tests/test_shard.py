@@ -57,6 +57,13 @@ def test_slice_batch_rebases_reads():
     ref = harness.synth_batch(3, 100, 300, 5, 10)
     assert np.array_equal(sub["depth"], ref["depth"]) and np.array_equal(sub["reads"], ref["reads"])
     assert len(shard.slice_batch(batch, 0, 700, 900)["ref"]) == 0
+    from popbam_amd import workload
+    p = workload.default_params(5)
+    kb, kref = harness.key_batch(b, p), harness.key_batch(ref, p)
+    ksub = shard.slice_batch(kb, 1000, 1100, 1300)
+    assert ksub["pos0"] == 1100
+    for f in ("ref", "k", "rmsq", "keys"):
+        assert np.array_equal(ksub[f], kref[f]), f
 
 
 def _oracle_block(st, b, e):
@@ -119,7 +126,7 @@ def test_gpu_blocks_on_rebased_pileups(gpu_lib, world):
             if reg is None:
                 continue
             lo, hi = shard.positions_needed(reg[0], reg[1], st.opts.win_size, windowed)
-            sub = shard.slice_batch(st.batch, 0, lo, max(hi, lo + 1))
+            sub = shard.slice_batch(st.kbatch, 0, lo, max(hi, lo + 1))
             parts.append(engine.run_command(st.opts, st.sm, st.chr, reg[0], reg[1], sub, pos0=sub["pos0"],
                                             refid=st.refid))
         ours = "".join(parts)
