@@ -392,21 +392,28 @@ SfsConst sfs_const(int n) {
     return k;
 }
 
+// the SFS of population i and its segregating-site count S (calc_sfs, pop_sfs.cpp:238-254)
+void sfs_bins(const orc_params *p, const orc_cmd *c, const Window &W, int i, std::vector<int> &sfs, int &S) {
+    sfs.assign(p->pop_n[i] + 1, 0);
+    S = 0;
+    for (int j = 0; j < W.segsites; j++) {
+        uint64_t t = W.types[W.idx[j]];
+        uint64_t pt = t & p->pop_mask[i];
+        unsigned short freq;
+        if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(p->pop_n[i] - popcnt64(pt));
+        else freq = (unsigned short)popcnt64(pt);
+        ++sfs[freq];
+        if (freq > 0 && freq < p->pop_n[i]) ++S;
+    }
+}
+
 void do_sfs(Out &o, const orc_params *p, const orc_cmd *c, const Window &W, const SfsConst &K) {
     int np = p->n_pops;
     std::vector<double> td(np, 0.0), fwh(np, 0.0);
     std::vector<int> num_snps(np, 0);
     for (int i = 0; i < np; i++) {
-        std::vector<int> sfs(p->pop_n[i] + 1, 0);
-        for (int j = 0; j < W.segsites; j++) {
-            uint64_t t = W.types[W.idx[j]];
-            uint64_t pt = t & p->pop_mask[i];
-            unsigned short freq;
-            if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(p->pop_n[i] - popcnt64(pt));
-            else freq = (unsigned short)popcnt64(pt);
-            ++sfs[freq];
-            if (freq > 0 && freq < p->pop_n[i]) ++num_snps[i];
-        }
+        std::vector<int> sfs;
+        sfs_bins(p, c, W, i, sfs, num_snps[i]);
         int n = p->pop_n[i];
         int S = num_snps[i];
         if (S > 0 && n > 1) {
@@ -1108,6 +1115,30 @@ long orc_windows_from_sites(const orc_params *p, const orc_cmd *c, const uint64_
     return finish(o, out, cap);
 }
 
+// SFS bins, S and Watterson's theta S / a1[n] per (window, population) -- calc_sfs's integers,
+// never printed by the reference (parity unpinned beyond the D / H they feed).
+long orc_sfs_windows(const orc_params *p, const orc_cmd *c, const uint64_t *types, const uint8_t *flags,
+                     uint32_t n_win, const int32_t *wbeg, const int32_t *wend, int stride, int32_t *bins,
+                     int32_t *seg_pop, double *theta_w) {
+    if (!p || !c) return -1;
+    SfsConst K = sfs_const(p->n_samples);
+    Window W;
+    const int np = p->n_pops;
+    for (uint32_t w = 0; w < n_win; w++) {
+        init_window(W, p, wbeg[w], wend[w]);
+        for (int pos = wbeg[w]; pos < wend[w]; pos++) add_site(W, p, (uint32_t)pos, types[pos], flags[pos], nullptr, 0);
+        for (int i = 0; i < np; i++) {
+            std::vector<int> sfs;
+            int S = 0;
+            sfs_bins(p, c, W, i, sfs, S);
+            for (int j = 0; j < stride; j++) bins[((size_t)w * np + i) * stride + j] = j < (int)sfs.size() ? sfs[j] : 0;
+            seg_pop[(size_t)w * np + i] = S;
+            theta_w[(size_t)w * np + i] = (double)S / K.a1[p->pop_n[i]];
+        }
+    }
+    return 0;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------- synthetic pileup
@@ -1128,7 +1159,7 @@ extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int3
     uint64_t h = sm64(seed ^ sm64(pos ^ ((uint64_t)(uint32_t)contig << 40)));
     int ref_idx = (int)(h & 3);
     int snp = ((h >> 2) & 0x3FF) < 12;
-    int alt = (ref_idx + 1 + (int)((h >> 12) % 3)) & 3;
+    int alt = (ref_idx + 1 + (int)((((h >> 12) & 0xFFFFu) * 3u) >> 16)) & 3;
     uint32_t f16 = (uint32_t)((h >> 16) & 0xFFFF);
     *ref = (uint8_t)"ACGT"[ref_idx];
     uint32_t nr = 0;
@@ -1145,8 +1176,8 @@ extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int3
         for (int r = 0; r < d; ++r) {
             uint64_t hr = sm64(hs + (uint64_t)r + 1);
             int base = (hr & 1) ? a1 : a0;
-            if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((hr >> 8) % 3)) & 3;
-            uint32_t bq = 20 + (uint32_t)((hr >> 16) % 21);
+            if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((((uint32_t)(hr >> 8) & 0xFFu) * 3u) >> 8)) & 3;
+            uint32_t bq = 20 + ((((uint32_t)(hr >> 16) & 0xFFFFu) * 21u) >> 16);
             uint32_t strand = (uint32_t)((hr >> 40) & 1);
             if (reads) reads[nr] = bq | (60u << 8) | ((1u << base) << 16) | (strand << 20);
             ++nr;

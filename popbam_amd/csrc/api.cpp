@@ -134,6 +134,17 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     d.min_baseQ = p->min_baseQ & 0xff;
     d.flag = p->flag;
     d.k16 = p->max_depth > 255 ? 1 : 0;
+    // population of each sample: assign_pops gives every sample one population (popbam.cpp:145-171)
+    for (int v = 0; v < PBG_MAX_SAMPLES; ++v) d.sample_pop[v] = -1;
+    for (int i = 0; i < p->n_pops; ++i)
+        for (int v = 0; v < p->n_samples; ++v)
+            if ((p->pop_mask[i] >> v) & 1) {
+                if (d.sample_pop[v] >= 0) {
+                    delete c;
+                    return fail(nullptr, PBG_E_ARG, "population masks overlap");
+                }
+                d.sample_pop[v] = (int8_t)i;
+            }
     d.sfs_stride = 1;
     for (int i = 0; i < p->n_pops; ++i) d.sfs_stride = std::max(d.sfs_stride, p->pop_n[i] + 1);
     auto bad = [&](hipError_t e, const char *what) {
@@ -340,6 +351,7 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
                      const pbg_stat_opts *o, const pbg_window_out *out, void *stream) {
     if (!c || !rows || !wins || !o || !out) return fail(c, PBG_E_ARG, "null argument");
     if (n_win == 0) return PBG_OK;
+    if ((uintptr_t)rows & 15) return fail(c, PBG_E_ARG, "rows must be 16-byte aligned");
     {
         const uint32_t ld = o->stats & (PBG_S_ZNS | PBG_S_OMEGA | PBG_S_WALL);
         if (ld & (ld - 1)) return fail(c, PBG_E_ARG, "at most one of ZnS / omega / Wall per call (shared outputs)");
@@ -352,26 +364,29 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     A.jc = o->jc;
     A.wins = wins;
     A.out = *out;
-    // global workspace: only for windows that outgrow LDS and for omega / Wall lists.  The
-    // plan is cached per device window list, so steady-state calls do not synchronise.
+    // global workspace: only for windows that outgrow LDS (longer than kSegCap rows) and for
+    // the omega / Wall lists.  The plan is cached per device window list, so steady-state calls
+    // do not synchronise.
+    const bool ld_ws = (o->stats & (PBG_S_OMEGA | PBG_S_WALL)) != 0;
     if (c->ws_key != (const void *)wins || c->ws_nwin != n_win || c->ws_nrows != n_rows || c->ws_stats != o->stats) {
         std::vector<pbg_window> hw(n_win);
         HIPCHK(c, hipMemcpyAsync(hw.data(), wins, n_win * sizeof(pbg_window), hipMemcpyDeviceToHost,
                                  (hipStream_t)stream));
         HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
-        int64_t maxlen = 0;
         std::vector<uint64_t> off(n_win);
         uint64_t tot = 0;
+        bool any = false;
         for (uint32_t i = 0; i < n_win; ++i) {
             if (hw[i].beg < 0 || hw[i].end < hw[i].beg || (uint32_t)hw[i].end > n_rows)
                 return fail(c, PBG_E_RANGE, "window outside the row range");
-            int64_t len = hw[i].end - hw[i].beg;
-            maxlen = std::max(maxlen, len);
+            const int64_t len = hw[i].end - hw[i].beg;
             off[i] = tot;
-            tot += pbg::ws_slice(len, c->dp.n, c->dp.npops);
+            if (ld_ws || len > pbg::kSegCap) {
+                tot += pbg::ws_slice(len, c->dp.n, c->dp.npops);
+                any = true;
+            }
         }
-        c->ws_need = (o->stats & (PBG_S_ZNS | PBG_S_OMEGA | PBG_S_WALL)) || maxlen > pbg::kSegCap ||
-                     (int64_t)c->dp.n * (maxlen / 64 + 1) > pbg::kPlaneCap;
+        c->ws_need = any;
         if (c->ws_need) {
             if (tot * 8 > c->ws_cap) {
                 if (c->d_ws) HIPCHK(c, hipFree(c->d_ws));
@@ -385,16 +400,16 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
                 HIPCHK(c, hipMalloc(&c->d_wsoff, n_win * 8));
                 c->wsoff_cap = n_win * 8;
             }
-            // seg_count [n_win] | var_count [n_win*np] | ld_ns [n_win*np]
-            const size_t segcnt_bytes = (size_t)n_win * (1 + 2 * (size_t)c->dp.npops) * 4;
-            if (segcnt_bytes > c->segcnt_cap) {
-                if (c->d_segcnt) HIPCHK(c, hipFree(c->d_segcnt));
-                c->d_segcnt = nullptr;
-                HIPCHK(c, hipMalloc((void **)&c->d_segcnt, segcnt_bytes));
-                c->segcnt_cap = segcnt_bytes;
-            }
             HIPCHK(c, hipMemcpyAsync(c->d_wsoff, off.data(), n_win * 8, hipMemcpyHostToDevice, (hipStream_t)stream));
             HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+        }
+        // seg_count [n_win] | var_count [n_win*np] | ld_ns [n_win*np]
+        const size_t segcnt_bytes = (size_t)n_win * (1 + 2 * (size_t)c->dp.npops) * 4;
+        if (segcnt_bytes > c->segcnt_cap) {
+            if (c->d_segcnt) HIPCHK(c, hipFree(c->d_segcnt));
+            c->d_segcnt = nullptr;
+            HIPCHK(c, hipMalloc((void **)&c->d_segcnt, segcnt_bytes));
+            c->segcnt_cap = segcnt_bytes;
         }
         c->ws_key = wins;
         c->ws_nwin = n_win;
@@ -404,10 +419,14 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     if (c->ws_need) {
         A.ws = c->d_ws;
         A.ws_off = c->d_wsoff;
-        A.seg_count = c->d_segcnt;
-        A.var_count = c->d_segcnt + n_win;
-        A.ld_ns = c->d_segcnt + n_win + (size_t)n_win * c->dp.npops;
     }
+    A.seg_count = c->d_segcnt;
+    A.var_count = c->d_segcnt + n_win;
+    A.ld_ns = c->d_segcnt + n_win + (size_t)n_win * c->dp.npops;
+    int r2_total = 0;
+    for (int i = 0; i < c->dp.npops; ++i) r2_total += (c->dp.pop_n[i] + 1) * (c->dp.pop_n[i] + 1) * (c->dp.pop_n[i] + 1);
+    A.lds = pbg::stats_lds_layout(c->dp.n, c->dp.npops, c->dp.sfs_stride, o->stats, r2_total);
+    if (A.lds.bytes > 64 * 1024) return fail(c, PBG_E_ARG, "statistics need more LDS than a workgroup has");
     HIPCHK(c, pbg::launch_window_stats(c->row_bytes, c->dp, c->dt, rows, n_rows, n_win, A, (hipStream_t)stream));
     return PBG_OK;
 }
@@ -512,7 +531,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         HIPCHK(c, d_rq.alloc(nt * 4));
         HIPCHK(c, d_boff.alloc((dblk + 1) * 8));
         HIPCHK(c, d_keys.alloc((r1 - r0) * 2));
-        HIPCHK(c, d_rows.alloc((size_t)dsites * rb));
+        HIPCHK(c, d_rows.alloc(((size_t)dsites * rb + 15) & ~(size_t)15));
         HIPCHK(c, hipMemcpy(d_ref.p, hp->ref + (size_t)blo * pbg::kSiteBlock, dsites, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(d_k.p, (const char *)hp->k + t0 * kb, nt * kb, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(d_rq.p, hp->rmsq + t0, nt * 4, hipMemcpyHostToDevice));

@@ -21,6 +21,7 @@ struct DevParams {
     uint32_t flag;
     int32_t k16;          // k[] is u16 (max_depth > 255), else u8
     int32_t sfs_stride;   // largest population + 1 (pbg_window_out.sfs_bins row)
+    int8_t sample_pop[PBG_MAX_SAMPLES];   // population of each sample (-1: none); masks are disjoint
 };
 
 // Host-built tables resident in HBM for the lifetime of a context.
@@ -62,7 +63,7 @@ __host__ __device__ inline SynthSite synth_site(uint64_t seed, int contig, uint6
     s.h = splitmix64(seed ^ splitmix64(pos ^ ((uint64_t)(uint32_t)contig << 40)));
     s.ref_idx = (int)(s.h & 3);
     s.snp = ((s.h >> 2) & 0x3FF) < 12;          // theta ~ 0.012
-    s.alt = (s.ref_idx + 1 + (int)((s.h >> 12) % 3)) & 3;
+    s.alt = (s.ref_idx + 1 + (int)((((s.h >> 12) & 0xFFFFu) * 3u) >> 16)) & 3;   // 1..3 steps away
     s.f16 = (uint32_t)((s.h >> 16) & 0xFFFF);   // derived allele frequency
     return s;
 }
@@ -81,18 +82,19 @@ __host__ __device__ inline uint32_t synth_read(const SynthSite &s, uint64_t hs, 
     int a1 = (s.snp && (uint32_t)((hs >> 16) & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
     uint64_t hr = splitmix64(hs + (uint64_t)r + 1);
     int base = (hr & 1) ? a1 : a0;
-    if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((hr >> 8) % 3)) & 3;   // ~0.8% errors
-    uint32_t bq = 20 + (uint32_t)((hr >> 16) % 21);                               // 20..40
+    // ~0.8 % errors; fixed-point ranges (no 64-bit division): other base 1..3 steps away, baseQ 20..40
+    if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((((uint32_t)(hr >> 8) & 0xFFu) * 3u) >> 8)) & 3;
+    uint32_t bq = 20 + ((((uint32_t)(hr >> 16) & 0xFFFFu) * 21u) >> 16);
     uint32_t strand = (uint32_t)((hr >> 40) & 1);
     return bq | (60u << 8) | ((1u << base) << 16) | (strand << 20);
 }
 __host__ __device__ inline uint8_t synth_ref_char(const SynthSite &s) { return (uint8_t)"ACGT"[s.ref_idx]; }
 
-constexpr int kSegCap = 2048;        // segregating rows kept in LDS per window
-constexpr int kPlaneCap = 1024;      // bitplane words kept in LDS (n * words)
+constexpr int kSegCap = 256;         // segregating rows kept in LDS per window (beyond: workspace)
+constexpr int kVarCap = 256;         // ZnS variable-site list kept in LDS per population
 
-// Per-window global workspace slice (u64 units), used only when a window outgrows LDS or
-// for the omega / Wall lists: [seg rows: len+1][bitplanes: n*(len/64+2)][lists: np*(len+1)]
+// Per-window global workspace slice (u64 units), planned by the host for windows longer than
+// kSegCap and for the omega / Wall lists: [seg rows: len+1][bitplanes: n*(len/64+2)][lists: np*(len+1)]
 __host__ __device__ inline uint64_t ws_plane_off(int64_t len) { return (uint64_t)len + 1; }
 __host__ __device__ inline uint64_t ws_list_off(int64_t len, int n) {
     return ws_plane_off(len) + (uint64_t)n * (uint64_t)(len / 64 + 2);
@@ -100,6 +102,15 @@ __host__ __device__ inline uint64_t ws_list_off(int64_t len, int n) {
 __host__ __device__ inline uint64_t ws_slice(int64_t len, int n, int np) {
     return ws_list_off(len, n) + (uint64_t)np * (uint64_t)(len + 1);
 }
+
+// Dynamic LDS of window_stats_kernel (one wave per window): byte offsets of its arrays, sized
+// by the host for the sample / population counts and the statistics asked for.
+struct WinLds {
+    uint32_t seg, var, plane, diff, acc, amin, bins, rbuf, r2, bytes;
+    int32_t planecap;   // bitplane words in LDS (n * kSegCap / 64)
+    int32_t r2lds;      // doubles of the r^2 tables copied to LDS (0: read from HBM / L2)
+};
+WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_total);
 
 struct StatsArgs {
     uint32_t stats;
@@ -111,6 +122,7 @@ struct StatsArgs {
     int32_t *var_count;              // [n_win*npops] ZnS: rows variable within the population
     int32_t *ld_ns;                  // [n_win*npops] ZnS: the reference's num_snps
     pbg_window_out out;
+    WinLds lds;
 };
 
 // Samples deeper than the register sort width (16 reads) are finished outside the main call

@@ -54,6 +54,9 @@ def oracle():
         lib.orc_windows_from_sites.restype = C.c_long
         lib.orc_windows_from_sites.argtypes = [P(OrcParams), P(OrcCmd), C.c_void_p, C.c_void_p, C.c_uint32,
                                                C.c_void_p, C.c_void_p, C.c_char_p, C.c_size_t]
+        lib.orc_sfs_windows.restype = C.c_long
+        lib.orc_sfs_windows.argtypes = [P(OrcParams), P(OrcCmd), C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                        C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.orc_synth_batch.restype = C.c_uint64
         lib.orc_synth_batch.argtypes = [C.c_uint64, C.c_int32, C.c_uint64, C.c_uint32, C.c_int32, C.c_int32,
                                         C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]

@@ -293,3 +293,58 @@ def test_fixture_rows_only_and_cb_paths_match_oracle(gpu_lib, name):
                    f"ref {st.batch['ref'][i]} depth {st.batch['depth'][i].tolist()}\nbad {bad[:40].tolist()}\n{detail(i)}")
             raise AssertionError(msg)
     ctx.close()
+
+
+@pytest.mark.parametrize("n,npops,flag,outidx", [(12, 2, 0, 0), (24, 3, 0x40, 5), (64, 4, 0x40, 63), (11, 1, 0, 0),
+                                                 (30, 5, 0, 0)])
+def test_sfs_bins_and_theta_w(gpu_lib, n, npops, flag, outidx):
+    """The SFS bins, S and theta_W = S / a1[n_pop] (north_star outputs the reference never prints;
+    parity unpinned) equal the oracle's calc_sfs integers, bit for bit, for every window layout,
+    with and without the outgroup flip."""
+    import torch
+    from popbam_amd import _lib, workload
+    ctx, params = _ctx(n, npops, flag=flag)
+    n_sites = 64 * 4000
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 3 * n)
+    rng = np.random.default_rng(n)
+    cuts = np.sort(rng.choice(n_sites, 30, replace=False))
+    wins = workload.reference_windows(0, n_sites, 10_000) + [(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
+    wins += [(0, n_sites), (9, 9)]
+    hp = workload.HotPath(ctx, syn, wins, _lib.PBG_S_SFS)
+    hp.opts.outidx = outidx
+    hp.step()
+    ctx.sync_check()
+    types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites)
+    stride = ctx.sfs_stride
+    nw = len(wins)
+    bins = np.zeros(nw * npops * stride, np.int32)
+    segp = np.zeros(nw * npops, np.int32)
+    tw = np.zeros(nw * npops, np.float64)
+    c = harness.OrcCmd()
+    c.outidx = outidx
+    wb = np.array([a for a, _ in wins], np.int32)
+    we = np.array([b for _, b in wins], np.int32)
+    assert harness.oracle().orc_sfs_windows(C.byref(harness.oracle_params_from(params)), C.byref(c),
+                                            types.ctypes.data, flags.ctypes.data, nw, wb.ctypes.data, we.ctypes.data,
+                                            stride, bins.ctypes.data, segp.ctypes.data, tw.ctypes.data) == 0
+    assert np.array_equal(hp.out.t["sfs_bins"].cpu().numpy(), bins)
+    assert np.array_equal(hp.out.t["seg_pop"].cpu().numpy(), segp)
+    assert np.array_equal(hp.out.t["theta_w"].cpu().numpy().view(np.uint64), tw.view(np.uint64))
+    assert segp.sum() > 0
+    ctx.close()
+
+
+def test_inconsistent_batch_is_reported(gpu_lib):
+    """pbg_call_sites on a batch whose block_off disagrees with k[]: the kernels never read past
+    the block's keys, write uncounted rows, and pbg_check reports PBG_E_BATCH (then clears)."""
+    import torch
+    from popbam_amd import _lib, workload
+    ctx, params = _ctx(12)
+    syn = workload.SynthPileup(ctx, 64 * 100, 10, SEED)
+    syn.block_off[5] += 3
+    hp = workload.HotPath(ctx, syn, [(0, 64 * 100)], 0)
+    for cb in (None, torch.zeros(64 * 100 * 12, dtype=torch.int64, device="cuda")):
+        hp.call(cb=cb)
+        assert ctx.lib.pbg_check(ctx.h, None) == _lib.PBG_E_BATCH
+        assert ctx.lib.pbg_check(ctx.h, None) == _lib.PBG_OK
+    ctx.close()

@@ -27,6 +27,11 @@ def per_kernel(path):
 
 def main():
     tag = sys.argv[1]
+    rnd = tag.split("s")[0] if tag.startswith("r") else "misc"
+    global PROF
+    top = PROF
+    PROF = os.path.join(top, rnd)
+    os.makedirs(PROF, exist_ok=True)
     shutil.copy(os.path.join(OUT, "prof_trace", "run_kernel_stats.csv"), os.path.join(PROF, f"{tag}_kernel_stats.csv"))
     bench = open(os.path.join(OUT, "bench.log")).read().strip().splitlines()[-1]
     b = json.loads(bench)
@@ -44,8 +49,8 @@ def main():
            "fetch_size_kib": fetch[k], "write_size_kib": write[k], "fetch_correction": 2.0,
            "hbm_bytes_per_launch": int(fetch[k] * 1024 * 2 + write[k] * 1024),
            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on bench.py --steps 2, {tag}",
-           "algorithmic_bytes_per_launch": b["roofline"]["bytes_per_launch"]}
-    json.dump(pmc, open(os.path.join(PROF, f"pmc_{k}.json"), "w"), indent=1)
+           "algorithmic_bytes_per_launch": b["roofline"]["bytes_per_launch"], "layout": "keys16"}
+    json.dump(pmc, open(os.path.join(top, f"pmc_{k}.json"), "w"), indent=1)
     print(json.dumps(pmc, indent=1))
 
 
