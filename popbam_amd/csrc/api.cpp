@@ -306,6 +306,7 @@ int pbg_check(pbg_ctx *c, void *stream) {
     HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (!herr) return PBG_OK;
     HIPCHK(c, hipMemset(c->d_err, 0, sizeof(int)));
+    if (herr & 4) return fail(c, PBG_E_RANGE, "statistics workspace exhausted (windows with very many segregating sites)");
     if (herr & 2) return fail(c, PBG_E_BATCH, "synthetic batch needs more keys than keys_cap");
     return fail(c, PBG_E_BATCH, "pileup block_off disagrees with k[]");
 }
@@ -364,47 +365,41 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     A.jc = o->jc;
     A.wins = wins;
     A.out = *out;
-    // global workspace: only for windows that outgrow LDS (longer than kSegCap rows) and for
-    // the omega / Wall lists.  The plan is cached per device window list, so steady-state calls
-    // do not synchronise.
+    // statistics workspace: a pool the windows take slices of on the device (windows with more
+    // than kSegCap segregating rows, omega / Wall lists, ZnS lists).  Sized from the window list
+    // (worst case, at most kPoolMax words); the plan is cached per device window list, so
+    // steady-state calls do not synchronise.
     const bool ld_ws = (o->stats & (PBG_S_OMEGA | PBG_S_WALL)) != 0;
+    const int n = c->dp.n, np = c->dp.npops;
     if (c->ws_key != (const void *)wins || c->ws_nwin != n_win || c->ws_nrows != n_rows || c->ws_stats != o->stats) {
         std::vector<pbg_window> hw(n_win);
         HIPCHK(c, hipMemcpyAsync(hw.data(), wins, n_win * sizeof(pbg_window), hipMemcpyDeviceToHost,
                                  (hipStream_t)stream));
         HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
-        std::vector<uint64_t> off(n_win);
-        uint64_t tot = 0;
-        bool any = false;
+        uint64_t worst = 0;
         for (uint32_t i = 0; i < n_win; ++i) {
             if (hw[i].beg < 0 || hw[i].end < hw[i].beg || (uint32_t)hw[i].end > n_rows)
                 return fail(c, PBG_E_RANGE, "window outside the row range");
-            const int64_t len = hw[i].end - hw[i].beg;
-            off[i] = tot;
-            if (ld_ws || len > pbg::kSegCap) {
-                tot += pbg::ws_slice(len, c->dp.n, c->dp.npops);
-                any = true;
-            }
+            const uint64_t len = (uint64_t)(hw[i].end - hw[i].beg);
+            if (ld_ws || len > (uint64_t)pbg::kSegCap) worst += len + (uint64_t)n * (len / 64 + 1) + (ld_ws ? np * len : 0);
+            if (o->stats & PBG_S_ZNS) worst += np * len;
         }
-        c->ws_need = any;
-        if (c->ws_need) {
-            if (tot * 8 > c->ws_cap) {
-                if (c->d_ws) HIPCHK(c, hipFree(c->d_ws));
-                c->d_ws = nullptr;
-                HIPCHK(c, hipMalloc(&c->d_ws, tot * 8));
-                c->ws_cap = tot * 8;
-            }
-            if (n_win * 8 > c->wsoff_cap) {
-                if (c->d_wsoff) HIPCHK(c, hipFree(c->d_wsoff));
-                c->d_wsoff = nullptr;
-                HIPCHK(c, hipMalloc(&c->d_wsoff, n_win * 8));
-                c->wsoff_cap = n_win * 8;
-            }
-            HIPCHK(c, hipMemcpyAsync(c->d_wsoff, off.data(), n_win * 8, hipMemcpyHostToDevice, (hipStream_t)stream));
-            HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+        constexpr uint64_t kPoolMax = 128ull << 20;   // words (1 GiB)
+        const uint64_t want = std::max<uint64_t>(1024, std::min(worst, kPoolMax));
+        if (want * 8 > c->ws_cap) {
+            if (c->d_ws) HIPCHK(c, hipFree(c->d_ws));
+            c->d_ws = nullptr;
+            HIPCHK(c, hipMalloc(&c->d_ws, want * 8));
+            c->ws_cap = want * 8;
+        }
+        if ((size_t)n_win * 16 + (size_t)n_win * np * 8 + 8 > c->wsoff_cap) {   // win_off | zoff | pool_used
+            if (c->d_wsoff) HIPCHK(c, hipFree(c->d_wsoff));
+            c->d_wsoff = nullptr;
+            c->wsoff_cap = (size_t)n_win * 16 + (size_t)n_win * np * 8 + 8;
+            HIPCHK(c, hipMalloc(&c->d_wsoff, c->wsoff_cap));
         }
         // seg_count [n_win] | var_count [n_win*np] | ld_ns [n_win*np]
-        const size_t segcnt_bytes = (size_t)n_win * (1 + 2 * (size_t)c->dp.npops) * 4;
+        const size_t segcnt_bytes = (size_t)n_win * (1 + 2 * (size_t)np) * 4;
         if (segcnt_bytes > c->segcnt_cap) {
             if (c->d_segcnt) HIPCHK(c, hipFree(c->d_segcnt));
             c->d_segcnt = nullptr;
@@ -416,16 +411,17 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
         c->ws_nrows = n_rows;
         c->ws_stats = o->stats;
     }
-    if (c->ws_need) {
-        A.ws = c->d_ws;
-        A.ws_off = c->d_wsoff;
-    }
+    A.pool = c->d_ws;
+    A.pool_cap = c->ws_cap / 8;
+    A.win_off = c->d_wsoff;
+    A.zoff = c->d_wsoff + 2 * (size_t)n_win;
+    A.pool_used = reinterpret_cast<unsigned long long *>(c->d_wsoff + 2 * (size_t)n_win + (size_t)n_win * np);
+    A.err = c->d_err;
+    HIPCHK(c, hipMemsetAsync(A.pool_used, 0, 8, (hipStream_t)stream));
     A.seg_count = c->d_segcnt;
     A.var_count = c->d_segcnt + n_win;
-    A.ld_ns = c->d_segcnt + n_win + (size_t)n_win * c->dp.npops;
-    int r2_total = 0;
-    for (int i = 0; i < c->dp.npops; ++i) r2_total += (c->dp.pop_n[i] + 1) * (c->dp.pop_n[i] + 1) * (c->dp.pop_n[i] + 1);
-    A.lds = pbg::stats_lds_layout(c->dp.n, c->dp.npops, c->dp.sfs_stride, o->stats, r2_total);
+    A.ld_ns = c->d_segcnt + n_win + (size_t)n_win * np;
+    A.lds = pbg::stats_lds_layout(n, np, c->dp.sfs_stride, o->stats, 0);
     if (A.lds.bytes > 64 * 1024) return fail(c, PBG_E_ARG, "statistics need more LDS than a workgroup has");
     HIPCHK(c, pbg::launch_window_stats(c->row_bytes, c->dp, c->dt, rows, n_rows, n_win, A, (hipStream_t)stream));
     return PBG_OK;
@@ -650,7 +646,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         }
         int rc = pbg_window_stats(c, rows_p, dsites, (const pbg_window *)d_win.p, nw, &so, &O, s);
         if (rc) return rc;
-        HIPCHK(c, hipDeviceSynchronize());
+        if ((rc = pbg_check(c, s))) return rc;
         std::vector<int32_t> h_ns(szw), h_seg(szw), h_i1(szp), h_i2(szp), h_i3(szq), h_td(szt);
         std::vector<double> h_d1(std::max(szq, std::max(szp, szn))), h_d2(std::max(szq, szp)), h_d3(szp);
         HIPCHK(c, hipMemcpy(h_ns.data(), o_ns.p, szw * 4, hipMemcpyDeviceToHost));

@@ -93,16 +93,6 @@ __host__ __device__ inline uint8_t synth_ref_char(const SynthSite &s) { return (
 constexpr int kSegCap = 256;         // segregating rows kept in LDS per window (beyond: workspace)
 constexpr int kVarCap = 256;         // ZnS variable-site list kept in LDS per population
 
-// Per-window global workspace slice (u64 units), planned by the host for windows longer than
-// kSegCap and for the omega / Wall lists: [seg rows: len+1][bitplanes: n*(len/64+2)][lists: np*(len+1)]
-__host__ __device__ inline uint64_t ws_plane_off(int64_t len) { return (uint64_t)len + 1; }
-__host__ __device__ inline uint64_t ws_list_off(int64_t len, int n) {
-    return ws_plane_off(len) + (uint64_t)n * (uint64_t)(len / 64 + 2);
-}
-__host__ __device__ inline uint64_t ws_slice(int64_t len, int n, int np) {
-    return ws_list_off(len, n) + (uint64_t)np * (uint64_t)(len + 1);
-}
-
 // Dynamic LDS of window_stats_kernel (one wave per window): byte offsets of its arrays, sized
 // by the host for the sample / population counts and the statistics asked for.
 struct WinLds {
@@ -116,11 +106,18 @@ struct StatsArgs {
     uint32_t stats;
     int32_t min_freq, outidx, jc;
     const pbg_window *wins;
-    const uint64_t *ws_off;          // per-window offset into ws (u64 units), for big windows
-    uint64_t *ws;                    // global workspace
-    int32_t *seg_count;              // per-window segregating-site count (LD chains)
-    int32_t *var_count;              // [n_win*npops] ZnS: rows variable within the population
-    int32_t *ld_ns;                  // [n_win*npops] ZnS: the reference's num_snps
+    // Statistics workspace: a pool the windows that need it take slices of with one atomic add
+    // (windows with more than kSegCap segregating rows, the omega / Wall lists, the ZnS lists);
+    // an exhausted pool sets err bit 4 (pbg_check -> PBG_E_RANGE).
+    uint64_t *pool;
+    uint64_t pool_cap;                    // u64 words
+    unsigned long long *pool_used;        // [1] words taken, zeroed per call
+    int *err;
+    uint64_t *win_off;                    // [2*n_win] pool offsets: seg rows, omega / Wall lists
+    uint64_t *zoff;                       // [n_win*npops] pool offset of each ZnS chain's list
+    int32_t *seg_count;                   // [n_win] segregating rows
+    int32_t *var_count;                   // [n_win*npops] ZnS: rows variable within the population
+    int32_t *ld_ns;                       // [n_win*npops] ZnS: the reference's num_snps
     pbg_window_out out;
     WinLds lds;
 };

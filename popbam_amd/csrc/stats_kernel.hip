@@ -81,7 +81,7 @@ WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_to
     const bool planes = stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE);
     const bool diff = stats & (PBG_S_NUCDIV | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE);
     L.seg = take(kSegCap * 8);
-    L.var = take((stats & PBG_S_ZNS) ? kVarCap * 8 : 0);
+    L.var = take(0);
     L.planecap = planes ? n * (kSegCap / 64) : 0;
     L.plane = take((uint32_t)L.planecap * 8);
     L.diff = take(diff ? (uint32_t)(n * n * 2) : 0);
@@ -89,9 +89,9 @@ WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_to
     L.amin = take((stats & PBG_S_HAP_DXY) ? (uint32_t)(np * np * 4) : 0);
     L.bins = take((stats & (PBG_S_SFS | PBG_S_DIV_POP | PBG_S_HAP_K | PBG_S_HAP_EHHS)) ? (uint32_t)(np * (sfs_stride + 2) * 4)
                                                                                        : 0);
-    L.rbuf = take((stats & PBG_S_ZNS) ? 72 * 8 : 0);
-    L.r2lds = ((stats & PBG_S_ZNS) && r2_total <= 1024) ? r2_total : 0;
-    L.r2 = take((uint32_t)L.r2lds * 8);
+    L.rbuf = take((stats & PBG_S_ZNS) ? (uint32_t)np * 4 : 0);   // ZnS: variable sites per population
+    L.r2lds = 0;                                                   // (r^2 tables: window_zns_kernel)
+    L.r2 = take(0);
     L.bytes = b + 16;
     return L;
 }
@@ -104,13 +104,12 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     if (w >= n_win) return;
     const WinLds &L = A.lds;
     uint64_t *s_seg = reinterpret_cast<uint64_t *>(sm + L.seg);
-    uint64_t *s_var = reinterpret_cast<uint64_t *>(sm + L.var);
     uint64_t *s_plane = reinterpret_cast<uint64_t *>(sm + L.plane);
     uint16_t *s_diff = reinterpret_cast<uint16_t *>(sm + L.diff);
     int32_t *s_acc = reinterpret_cast<int32_t *>(sm + L.acc);
     int32_t *s_amin = reinterpret_cast<int32_t *>(sm + L.amin);
     int32_t *s_bins = reinterpret_cast<int32_t *>(sm + L.bins);
-    double *s_rbuf = reinterpret_cast<double *>(sm + L.rbuf);
+    int32_t *s_vc = reinterpret_cast<int32_t *>(sm + L.rbuf);
     double *s_r2 = reinterpret_cast<double *>(sm + L.r2);
     __shared__ int32_t s_misc[4];
 
@@ -118,19 +117,15 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     const int lane = threadIdx.x;
     const uint32_t stats = A.stats;
     const int64_t wb = A.wins[w].beg, we = A.wins[w].end > A.wins[w].beg ? A.wins[w].end : A.wins[w].beg;
-    const int64_t len = we - wb;
-    uint64_t *ws = A.ws ? A.ws + A.ws_off[w] : nullptr;          // planned for long windows / LD lists
     const bool ld_ws = (stats & (PBG_S_OMEGA | PBG_S_WALL)) != 0;  // window_ld_kernel reads the seg list
     for (int i = lane; i < L.r2lds; i += 64) s_r2[i] = T.r2[i];
 
-    // ---- one pass over the rows: counted total, ordered compaction of the segregating rows
+    // ---- pass over the rows: counted total, ordered compaction of the segregating rows (the
+    // first kSegCap into LDS)
     constexpr int R = 16 / RB;
     const uint4 *rw = reinterpret_cast<const uint4 *>(rows);
     const int64_t c0 = wb / R, c1 = (we + R - 1) / R;
-    int my_counted = 0;
-    uint32_t S = 0;
-    for (int64_t cb = c0; cb < c1; cb += 64) {
-        const int64_t c = cb + lane;
+    auto load_word = [&](int64_t c) -> uint4 {
         uint4 q = make_uint4(0, 0, 0, 0);
         if (c < c1) {
             if ((c + 1) * R <= (int64_t)n_rows) {
@@ -143,32 +138,79 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                 q = make_uint4(wd[0], wd[1], wd[2], wd[3]);
             }
         }
-        uint64_t t[R];
-        uint32_t segm = 0;
+        return q;
+    };
+    // seg rows of word c (in window): bit mask + types; `store` gets (index, types)
+    auto compact = [&](uint64_t *dst, uint32_t cap, bool count_sites, int &my_counted) -> uint32_t {
+        uint32_t S = 0;
+        for (int64_t cb = c0; cb < c1; cb += 64) {
+            const int64_t c = cb + lane;
+            const uint4 q = load_word(c);
+            uint64_t t[R];
+            uint32_t segm = 0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int64_t i = c * R + r;
-            bool cnt, sg;
-            row_in_word<RB>(q, r, t[r], cnt, sg);
-            const bool in = c < c1 && i >= wb && i < we;
-            my_counted += (in && cnt) ? 1 : 0;
-            segm |= (in && sg) ? (1u << r) : 0u;
-        }
-        const uint32_t ls = (uint32_t)__popc(segm);
-        const uint32_t incl = wave_incl_scan_s(ls);
-        uint32_t j = S + incl - ls;
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if ((segm >> r) & 1u) {
-                if (j < (uint32_t)kSegCap) s_seg[j] = t[r];
-                if (ws && (ld_ws || j >= (uint32_t)kSegCap)) ws[j] = t[r];
-                ++j;
+            for (int r = 0; r < R; ++r) {
+                const int64_t i = c * R + r;
+                bool cnt, sg;
+                row_in_word<RB>(q, r, t[r], cnt, sg);
+                const bool in = c < c1 && i >= wb && i < we;
+                if (count_sites) my_counted += (in && cnt) ? 1 : 0;
+                segm |= (in && sg) ? (1u << r) : 0u;
             }
-        S += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    }
+            const uint32_t ls = (uint32_t)__popc(segm);
+            const uint32_t incl = wave_incl_scan_s(ls);
+            uint32_t j = S + incl - ls;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if ((segm >> r) & 1u) {
+                    if (j < cap) dst[j] = t[r];
+                    ++j;
+                }
+            S += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        return S;
+    };
+    int my_counted = 0;
+    const uint32_t S = compact(s_seg, (uint32_t)kSegCap, true, my_counted);
     const int num_sites = wave_sum(my_counted);
+    const int nwords = S > 0 ? (int)((S + 63) / 64) : 1;
+    const bool need_planes = (stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY |
+                                       PBG_S_TREE)) != 0;
+    const bool need_diff = (stats & (PBG_S_NUCDIV | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE)) != 0;
+    // pool slice: [seg rows: S][bitplanes: n*nwords, when they outgrow LDS][omega / Wall lists: np*S]
+    const bool over = S > (uint32_t)kSegCap;
+    uint64_t *wsg = nullptr, *wpl = nullptr;
+    if (over || ld_ws) {
+        const uint64_t npl = (over && need_planes) ? (uint64_t)n * nwords : 0, nli = ld_ws ? (uint64_t)np * S : 0;
+        const uint64_t size = S + npl + nli;
+        unsigned long long off = 0;
+        if (lane == 0) {
+            off = atomicAdd(A.pool_used, (unsigned long long)size);
+            if (off + size > A.pool_cap) {
+                atomicOr(A.err, 4);
+                off = ~0ULL;
+            } else {
+                A.win_off[2 * w] = off;
+                A.win_off[2 * w + 1] = off + S + npl;
+            }
+        }
+        off = __shfl(off, 0, 64);
+        if (off == ~0ULL) {   // pool exhausted: reported by pbg_check, this window's outputs unset
+            if (lane == 0 && A.seg_count) A.seg_count[w] = 0;
+            return;
+        }
+        wsg = A.pool + off;
+        wpl = wsg + S;
+        __syncthreads();
+        if (over) {
+            int unused = 0;
+            (void)compact(wsg, S, false, unused);   // second pass, only for windows beyond kSegCap
+        } else {
+            for (uint32_t j = (uint32_t)lane; j < S; j += 64) wsg[j] = s_seg[j];
+        }
+    }
     __syncthreads();
-    auto seg_at = [&](uint32_t j) -> uint64_t { return j < (uint32_t)kSegCap ? s_seg[j] : ws[j]; };
+    auto seg_at = [&](uint32_t j) -> uint64_t { return j < (uint32_t)kSegCap ? s_seg[j] : wsg[j]; };
 
     const pbg_window_out &O = A.out;
     if (lane == 0) {
@@ -179,13 +221,9 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     const int npairs = np * (np - 1);
 
     // ---- bitplanes (hap.seq) and the u16 pairwise-difference matrix
-    const int nwords = S > 0 ? (int)((S + 63) / 64) : 1;
-    const bool need_planes = (stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY |
-                                       PBG_S_TREE)) != 0;
-    const bool need_diff = (stats & (PBG_S_NUCDIV | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE)) != 0;
     uint64_t *plane = nullptr;
     if (need_planes) {
-        plane = (n * nwords <= L.planecap) ? s_plane : ws + ws_plane_off(len);
+        plane = (n * nwords <= L.planecap) ? s_plane : wpl;
         // plane[v*nwords + k] bit b = sample v derived at segregating site 64k+b (hap.seq)
         for (int k = 0; k < nwords; ++k) {
             const uint32_t j = (uint32_t)(k * 64 + lane);
@@ -308,18 +346,59 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         if (O.div_pop) O.div_pop[(size_t)w * np + i] = x86nan(v);
     }
 
-    // ---- ld -o 0 (calc_zns, pop_ld.cpp:201-252): per population, the ordered list of
-    // segregating rows variable within it and num_snps (variable sites among the first S-1, plus
-    // the final unconditional increment); then the sum of r^2 over all pairs a < b of the list in
-    // the reference's order: all lanes compute the next 64 r^2 values of row a (zero-padded into
-    // LDS), lane 0 adds them in order (a +0.0 pad leaves a sum of r^2 >= +0 bit-unchanged)
+    // ---- ld -o 0 (calc_zns, pop_ld.cpp:201-252): per population, the ordered list of the
+    // segregating rows variable within it (masked to the population) goes to the pool for
+    // window_zns_kernel, with num_snps (variable sites among the first S-1, plus the final
+    // unconditional increment)
     if (stats & PBG_S_ZNS) {
+        // counts first (one pool allocation per window), then the lists
+        uint32_t tot = 0;
         for (int i = 0; i < np; ++i) {
             const uint64_t pm = P.pop_mask[i];
-            const int nn = P.pop_n[i], mf = A.min_freq, np1 = nn + 1;
-            uint64_t *wl = ws ? ws + ws_list_off(len, n) + (uint64_t)i * (uint64_t)(len + 1) : nullptr;
+            const int nn = P.pop_n[i], mf = A.min_freq;
             uint32_t V = 0;
             int lastvar = 0;
+            for (uint32_t c0 = 0; c0 < S; c0 += 64) {
+                const uint32_t j = c0 + (uint32_t)lane;
+                bool v = false;
+                if (j < S) {
+                    const int m = (int)pc(seg_at(j) & pm);
+                    v = m >= mf && m <= nn - mf;
+                    if (j == S - 1) lastvar = v ? 1 : 0;
+                }
+                V += (uint32_t)__popcll(__ballot(v));
+            }
+            lastvar = wave_sum(lastvar);
+            if (lane == 0) {
+                const int ns = S >= 1 ? (int)V - lastvar + 1 : 0;
+                s_vc[i] = (int)V;
+                A.var_count[(size_t)w * np + i] = (int)V;
+                A.ld_ns[(size_t)w * np + i] = ns;
+                if (O.ld_snps) O.ld_snps[(size_t)w * np + i] = ns;
+            }
+            tot += V;
+        }
+        unsigned long long off = 0;
+        if (lane == 0 && tot) {
+            off = atomicAdd(A.pool_used, (unsigned long long)tot);
+            if (off + tot > A.pool_cap) {
+                atomicOr(A.err, 4);
+                off = ~0ULL;
+            }
+        }
+        off = __shfl(off, 0, 64);
+        __syncthreads();
+        for (int i = 0; i < np; ++i) {
+            const uint64_t pm = P.pop_mask[i];
+            const int nn = P.pop_n[i], mf = A.min_freq;
+            const uint32_t Vi = (uint32_t)s_vc[i];
+            if (lane == 0) A.zoff[(size_t)w * np + i] = off;
+            if (off == ~0ULL) {   // pool exhausted: the chain sums nothing (err reported)
+                if (lane == 0) A.var_count[(size_t)w * np + i] = 0;
+                continue;
+            }
+            uint64_t *vl = A.pool + off;
+            uint32_t V = 0;
             for (uint32_t c0 = 0; c0 < S; c0 += 64) {
                 const uint32_t j = c0 + (uint32_t)lane;
                 uint64_t t = 0;
@@ -328,57 +407,12 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                     t = seg_at(j) & pm;
                     const int m = (int)pc(t);
                     v = m >= mf && m <= nn - mf;
-                    if (j == S - 1) lastvar = v ? 1 : 0;
                 }
                 const uint64_t bm = __ballot(v);
-                const uint32_t idx = V + (uint32_t)__popcll(bm & ((1ULL << lane) - 1));
-                if (v) {
-                    if (idx < (uint32_t)kVarCap) s_var[idx] = t;
-                    else wl[idx] = t;
-                }
+                if (v) vl[V + (uint32_t)__popcll(bm & ((1ULL << lane) - 1))] = t;
                 V += (uint32_t)__popcll(bm);
             }
-            lastvar = wave_sum(lastvar);
-            __syncthreads();
-            auto var_at = [&](uint32_t a) -> uint64_t { return a < (uint32_t)kVarCap ? s_var[a] : wl[a]; };
-            const double *r2p = (L.r2lds ? s_r2 : T.r2) + T.r2_off[i];
-            if (lane < 8) s_rbuf[64 + lane] = 0.0;
-            double acc = 0.0;
-            for (uint32_t a = 0; a + 1 < V; ++a) {
-                const uint64_t ta = var_at(a);
-                const int ma = (int)pc(ta);
-                for (uint32_t b0 = a + 1; b0 < V; b0 += 64) {
-                    const uint32_t b = b0 + (uint32_t)lane;
-                    double r = 0.0;
-                    if (b < V) {
-                        const uint64_t tb = var_at(b);
-                        r = r2p[(ma * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
-                    }
-                    s_rbuf[lane] = r;
-                    __syncthreads();
-                    if (lane == 0) {
-                        const uint32_t seg = min(64u, V - b0);
-                        for (uint32_t l = 0; l < seg; l += 8) {
-                            double x[8];
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) x[u] = s_rbuf[l + u];
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) acc += x[u];
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-            if (lane == 0) {
-                const int ns = S >= 1 ? (int)V - lastvar + 1 : 0;
-                double val = 0.0;
-                if (S >= 1) val = acc * (2.0 / (ns * (ns - 1)));
-                if (A.var_count) A.var_count[(size_t)w * np + i] = (int)V;
-                if (A.ld_ns) A.ld_ns[(size_t)w * np + i] = ns;
-                if (O.ld_snps) O.ld_snps[(size_t)w * np + i] = ns;
-                if (O.ld_val) O.ld_val[(size_t)w * np + i] = x86nan(val);
-            }
-            __syncthreads();
+            off += Vi;
         }
     }
 
@@ -476,12 +510,12 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     (void)s_misc;
 }
 
-// Serial LD chains, one lane per chain (pop_ld.cpp:201-458), reading the ordered segregating
-// lists window_stats_kernel compacted into the workspace.  Lanes of a wave belong to
+// Serial LD chains, one lane per chain (pop_ld.cpp:254-458), reading the ordered segregating
+// lists window_stats_kernel copied into the pool.  Lanes of a wave belong to
 // different windows, so the dependent double additions of 64 chains overlap.
 __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A) {
     __shared__ double s_r2[4096];
-    const int n = P.n, np = P.npops;
+    const int np = P.npops;
     int r2_total = 0;
     for (int i = 0; i < np; ++i) r2_total += (P.pop_n[i] + 1) * (P.pop_n[i] + 1) * (P.pop_n[i] + 1);
     const bool r2_lds = r2_total <= 4096;
@@ -495,19 +529,18 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
         // one chain per window: last_type is shared by all populations (Appendix A.9)
         const uint32_t w = gid;
         if (w >= n_win) return;
-        const int64_t len = A.wins[w].end > A.wins[w].beg ? A.wins[w].end - A.wins[w].beg : 0;
         const int S = A.seg_count[w];
-        const uint64_t *seg = A.ws + A.ws_off[w];
+        const uint64_t *seg = A.pool + A.win_off[2 * w];
         int ns[PBG_MAX_POPS], cong[PBG_MAX_POPS], part[PBG_MAX_POPS], nu[PBG_MAX_POPS];
         for (int j = 0; j < np; j++) ns[j] = cong[j] = part[j] = nu[j] = 0;
-        uint64_t *uniq = A.ws + A.ws_off[w] + ws_list_off(len, n);   // np slices of (len+1)
+        uint64_t *uniq = A.pool + A.win_off[2 * w + 1];   // np slices of S
         uint64_t last_type = 0;
         for (int i = 0; i < S; i++) {
             const uint64_t t = seg[i];
             for (int j = 0; j < np; j++) {
                 const uint64_t type = t & P.pop_mask[j];
                 const uint64_t comp = ~t & P.pop_mask[j];
-                uint64_t *u = uniq + (uint64_t)j * (uint64_t)(len + 1);
+                uint64_t *u = uniq + (uint64_t)j * (uint64_t)S;
                 if (type > 0 && type < P.pop_mask[j]) {
                     if (ns[j] == 0) {
                         u[nu[j]++] = type;
@@ -544,9 +577,8 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
     if (gid >= n_win * (uint32_t)np) return;
     const uint32_t w = gid / np;
     const int i = (int)(gid - w * np);
-    const int64_t len = A.wins[w].end > A.wins[w].beg ? A.wins[w].end - A.wins[w].beg : 0;
     const int S = A.seg_count[w];
-    const uint64_t *seg = A.ws + A.ws_off[w];
+    const uint64_t *seg = A.pool + A.win_off[2 * w];
     const int nn = P.pop_n[i], np1 = nn + 1, mf = A.min_freq;
     const uint64_t pm = P.pop_mask[i];
     const double *r2p = r2tab + T.r2_off[i];
@@ -556,7 +588,7 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
     {   // calc_omegamax pop_ld.cpp:254-373 (sums accumulate across partitions, A.8)
         if (S >= 1) {
             int V = 0;
-            uint64_t *vt = A.ws + A.ws_off[w] + ws_list_off(len, n) + (uint64_t)i * (uint64_t)(len + 1);
+            uint64_t *vt = A.pool + A.win_off[2 * w + 1] + (uint64_t)i * (uint64_t)S;
             for (int j = 0; j < S; j++) {
                 const uint64_t t = seg[j] & pm;
                 if (variable(pc(t))) {
@@ -589,6 +621,105 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
     if (O.ld_val) O.ld_val[(size_t)w * np + i] = x86nan(val);
 }
 
+// ZnS sums (calc_zns, pop_ld.cpp:215-248): a quad of lanes per (window, population) chain, 16
+// chains per wave.  The chain is the reference's exact sequence of additions over the pairs
+// a < b of the population's variable sites (a ascending, then b).  Each step the quad's four
+// lanes compute the r^2 of the next four pairs in parallel (the host's table, the reference's
+// own expression per (marg1, marg2, c11)), DPP quad broadcasts hand all four values to every
+// lane of the quad, and each lane adds them in pair order to the same running double -- so the
+// sum is bit-identical while the r^2 work runs 4-wide.  Pairs past the end add +0.0, which
+// leaves a sum of r^2 >= +0 unchanged.
+template <int K>
+__device__ __forceinline__ double quad_bcast(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), K * 0x55, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), K * 0x55, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+constexpr int kZnsStage = 256;   // list entries of a chain staged in LDS (longer lists: read from the pool)
+constexpr int kZnsUnroll = 4;    // steps whose loads are issued before their adds (latency hiding)
+constexpr int kZnsStride = kZnsStage + 2;   // u64 per chain slot: +16 B staggers the slots' LDS banks
+__global__ __launch_bounds__(64) void window_zns_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A,
+                                                        int r2_lds) {
+    extern __shared__ __align__(16) double s_dyn[];
+    double *s_r2t = s_dyn;                                                      // [r2_lds]
+    uint64_t *s_t = reinterpret_cast<uint64_t *>(s_dyn + r2_lds);              // [16][kZnsStride] types
+    for (int i = threadIdx.x; i < r2_lds; i += 64) s_r2t[i] = T.r2[i];
+    const int np = P.npops;
+    const int lane = threadIdx.x, g = lane & 3, q = lane >> 2;
+    const uint32_t nch = n_win * (uint32_t)np;
+    const uint32_t ch = blockIdx.x * 16 + (uint32_t)q;
+    int V = 0;
+    const uint64_t *L = A.pool;
+    int np1 = 1, r2o = 0;
+    if (ch < nch) {
+        const uint32_t w = ch / (uint32_t)np;
+        const int i = (int)(ch - w * (uint32_t)np);
+        V = A.var_count[ch];
+        L = A.pool + A.zoff[ch];
+        np1 = P.pop_n[i] + 1;
+        r2o = T.r2_off[i];
+    }
+    // all chains of the wave staged in LDS, or all read from the pool (wave-uniform, so every
+    // load below has a known address space: ds_read, not flat)
+    const bool staged = !__ballot(V > kZnsStage);
+    uint64_t *lt = s_t + q * kZnsStride;
+    if (staged)
+        for (int j = g; j < V; j += 4) lt[j] = L[j];
+    __syncthreads();
+    // row a, pairs b = b0 + g (b0 = a+1, a+5, ...); lanes past the row end add +0.0.  Branch-free:
+    // every step's list loads depend only on the (a, b0) arithmetic, so the loads of all
+    // kZnsUnroll steps issue before the first add waits on them.
+    auto run = [&](const uint64_t *lst, const double *r2p) -> double {
+        const int vm1 = V > 0 ? V - 1 : 0;
+        int a = 0, b0 = 1;
+        double acc = 0.0;
+        while (__ballot(a < V - 1)) {   // wave-uniform: until every chain of the wave is done
+            int ia[kZnsUnroll], ib[kZnsUnroll];
+            bool ok[kZnsUnroll];
+#pragma unroll
+            for (int u = 0; u < kZnsUnroll; ++u) {
+                const int b = b0 + g;
+                ok[u] = (a < V - 1) & (b < V);
+                ia[u] = min(a, vm1);
+                ib[u] = min(b, vm1);
+                b0 += 4;
+                const bool nxt = (b0 >= V) & (a < V - 1);
+                a += nxt ? 1 : 0;
+                b0 = nxt ? a + 1 : b0;
+            }
+            double r[kZnsUnroll];
+#pragma unroll
+            for (int u = 0; u < kZnsUnroll; ++u) {
+                const uint64_t ta = lst[ia[u]], tb = lst[ib[u]];
+                const double rv = r2p[((int)__popcll(ta) * np1 + (int)__popcll(tb)) * np1 + (int)__popcll(ta & tb)];
+                r[u] = ok[u] ? rv : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < kZnsUnroll; ++u) {   // pair order: step u's four pairs, lane 0..3
+                const double v0 = quad_bcast<0>(r[u]), v1 = quad_bcast<1>(r[u]), v2 = quad_bcast<2>(r[u]),
+                             v3 = quad_bcast<3>(r[u]);
+                acc += v0;
+                acc += v1;
+                acc += v2;
+                acc += v3;
+            }
+        }
+        return acc;
+    };
+    double acc;
+    if (staged) acc = r2_lds ? run(lt, s_r2t + r2o) : run(lt, T.r2 + r2o);
+    else acc = r2_lds ? run(L, s_r2t + r2o) : run(L, T.r2 + r2o);
+    if (g == 0 && ch < nch) {
+        const uint32_t w = ch / (uint32_t)np;
+        double val = 0.0;
+        if (A.seg_count[w] >= 1) {
+            const int ns = A.ld_ns[ch];
+            val = acc * (2.0 / (ns * (ns - 1)));
+        }
+        if (A.out.ld_val) A.out.ld_val[ch] = x86nan(val);
+    }
+}
+
 template __global__ void window_stats_kernel<2>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
 template __global__ void window_stats_kernel<4>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
 template __global__ void window_stats_kernel<8>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
@@ -604,6 +735,14 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
         case 4: hipLaunchKernelGGL(window_stats_kernel<4>, g, b, lds, stream, P, T, rows, n_rows, n_win, A); break;
         case 8: hipLaunchKernelGGL(window_stats_kernel<8>, g, b, lds, stream, P, T, rows, n_rows, n_win, A); break;
         default: hipLaunchKernelGGL(window_stats_kernel<16>, g, b, lds, stream, P, T, rows, n_rows, n_win, A); break;
+    }
+    if (A.stats & PBG_S_ZNS) {
+        int r2_total = 0;
+        for (int i = 0; i < P.npops; ++i) r2_total += (P.pop_n[i] + 1) * (P.pop_n[i] + 1) * (P.pop_n[i] + 1);
+        const int r2_lds = r2_total <= 4608 ? r2_total : 0;   // <= 36 KB of LDS per wave
+        const uint32_t chains = n_win * (uint32_t)P.npops;
+        const size_t lds = (size_t)r2_lds * sizeof(double) + 16 * kZnsStride * 8;
+        hipLaunchKernelGGL(window_zns_kernel, dim3((chains + 15) / 16), dim3(64), lds, stream, P, T, n_win, A, r2_lds);
     }
     const uint32_t ld = A.stats & (PBG_S_OMEGA | PBG_S_WALL);
     if (ld) {
