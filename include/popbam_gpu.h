@@ -185,7 +185,7 @@ int pbg_window_stats(pbg_ctx *ctx, const void *rows, uint32_t n_rows, const pbg_
 /* Waits for `stream` and reports what the kernels flagged since the last check: PBG_OK;
  * PBG_E_BATCH when a pileup batch's block_off disagreed with its k[] (the affected blocks
  * were written as uncounted rows and never read past their key range); PBG_E_RANGE when the
- * statistics workspace (windows with more than 256 segregating sites, LD lists; up to 1 GiB)
+ * statistics workspace (windows with more than 256 segregating sites, LD lists; up to 4 GiB)
  * ran out -- the windows that could not get a slice have unset outputs. */
 int pbg_check(pbg_ctx *ctx, void *stream);
 

@@ -1174,11 +1174,16 @@ extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int3
         int a0 = (snp && (uint32_t)(hs & 0xFFFF) < f16) ? alt : ref_idx;
         int a1 = (snp && (uint32_t)((hs >> 16) & 0xFFFF) < f16) ? alt : ref_idx;
         for (int r = 0; r < d; ++r) {
-            uint64_t hr = sm64(hs + (uint64_t)r + 1);
+            uint32_t hr = (uint32_t)(hs >> 32) ^ (0x9E3779B9u * (uint32_t)(r + 1));   // mix32 (lowbias32)
+            hr ^= hr >> 16;
+            hr *= 0x7FEB352Du;
+            hr ^= hr >> 15;
+            hr *= 0x846CA68Bu;
+            hr ^= hr >> 16;
             int base = (hr & 1) ? a1 : a0;
-            if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((((uint32_t)(hr >> 8) & 0xFFu) * 3u) >> 8)) & 3;
-            uint32_t bq = 20 + ((((uint32_t)(hr >> 16) & 0xFFFFu) * 21u) >> 16);
-            uint32_t strand = (uint32_t)((hr >> 40) & 1);
+            if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((((hr >> 8) & 0xFFu) * 3u) >> 8)) & 3;
+            uint32_t bq = 20 + ((((hr >> 16) & 0xFFFFu) * 21u) >> 16);
+            uint32_t strand = ((hr >> 8) ^ (hr >> 17)) & 1u;
             if (reads) reads[nr] = bq | (60u << 8) | ((1u << base) << 16) | (strand << 20);
             ++nr;
         }

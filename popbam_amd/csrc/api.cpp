@@ -31,10 +31,12 @@ struct pbg_ctx {
     // calls on the same resident batch do not synchronise
     const void *cap_key = nullptr;
     uint32_t cap_sites = 0, cap_val = 0;
-    // per-window-list workspace plan (keyed by the device window array)
-    const void *ws_key = nullptr;
-    uint32_t ws_nwin = 0, ws_nrows = 0, ws_stats = 0;
-    bool ws_need = false;
+    // window lists already validated (device pointer, size, rows, statistics), most recent last
+    struct Plan {
+        const void *wins;
+        uint32_t n_win, n_rows, stats;
+    };
+    std::vector<Plan> plans;
     uint64_t *d_ws = nullptr, *d_wsoff = nullptr;
     size_t ws_cap = 0, wsoff_cap = 0, segcnt_cap = 0;
     int32_t *d_segcnt = nullptr;
@@ -371,7 +373,10 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     // steady-state calls do not synchronise.
     const bool ld_ws = (o->stats & (PBG_S_OMEGA | PBG_S_WALL)) != 0;
     const int n = c->dp.n, np = c->dp.npops;
-    if (c->ws_key != (const void *)wins || c->ws_nwin != n_win || c->ws_nrows != n_rows || c->ws_stats != o->stats) {
+    bool known = false;
+    for (const auto &pl : c->plans)
+        known |= pl.wins == (const void *)wins && pl.n_win == n_win && pl.n_rows == n_rows && pl.stats == o->stats;
+    if (!known) {
         std::vector<pbg_window> hw(n_win);
         HIPCHK(c, hipMemcpyAsync(hw.data(), wins, n_win * sizeof(pbg_window), hipMemcpyDeviceToHost,
                                  (hipStream_t)stream));
@@ -384,7 +389,7 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
             if (ld_ws || len > (uint64_t)pbg::kSegCap) worst += len + (uint64_t)n * (len / 64 + 1) + (ld_ws ? np * len : 0);
             if (o->stats & PBG_S_ZNS) worst += np * len;
         }
-        constexpr uint64_t kPoolMax = 128ull << 20;   // words (1 GiB)
+        constexpr uint64_t kPoolMax = 512ull << 20;   // words (4 GiB)
         const uint64_t want = std::max<uint64_t>(1024, std::min(worst, kPoolMax));
         if (want * 8 > c->ws_cap) {
             if (c->d_ws) HIPCHK(c, hipFree(c->d_ws));
@@ -406,10 +411,8 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
             HIPCHK(c, hipMalloc((void **)&c->d_segcnt, segcnt_bytes));
             c->segcnt_cap = segcnt_bytes;
         }
-        c->ws_key = wins;
-        c->ws_nwin = n_win;
-        c->ws_nrows = n_rows;
-        c->ws_stats = o->stats;
+        if (c->plans.size() >= 16) c->plans.erase(c->plans.begin());
+        c->plans.push_back({wins, n_win, n_rows, o->stats});
     }
     A.pool = c->d_ws;
     A.pool_cap = c->ws_cap / 8;
@@ -464,7 +467,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
     HIPCHK(c, hipSetDevice(c->device));
     c->text.clear();
     c->cap_key = nullptr;   // this call's buffers are fresh allocations: drop cached plans
-    c->ws_key = nullptr;
+    c->plans.clear();
     const int n = c->dp.n, np = c->dp.npops;
     // ---- windows in contig coordinates (main_<cmd>)
     std::vector<std::pair<int32_t, int32_t>> win;

@@ -77,16 +77,32 @@ __host__ __device__ inline int synth_depth(uint64_t hs, int mean_depth) {
     uint64_t m = nb >= 64 ? ~0ULL : ((1ULL << nb) - 1);
     return __builtin_popcountll(bits & m);
 }
+// 32-bit finaliser (lowbias32) for the per-read draws: one per read, ~4x cheaper than splitmix64
+__host__ __device__ inline uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
 __host__ __device__ inline uint32_t synth_read(const SynthSite &s, uint64_t hs, int r) {
     int a0 = (s.snp && (uint32_t)(hs & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
     int a1 = (s.snp && (uint32_t)((hs >> 16) & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
-    uint64_t hr = splitmix64(hs + (uint64_t)r + 1);
+    // read r's 32 random bits: haplotype (bit 0), error (bits 1-7 all zero: 1/128), error base
+    // (bits 8-15), baseQ (bits 16-31), strand (bit 8 ^ bit 17)
+    const uint32_t hr = mix32((uint32_t)(hs >> 32) ^ (0x9E3779B9u * (uint32_t)(r + 1)));
     int base = (hr & 1) ? a1 : a0;
-    // ~0.8 % errors; fixed-point ranges (no 64-bit division): other base 1..3 steps away, baseQ 20..40
-    if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((((uint32_t)(hr >> 8) & 0xFFu) * 3u) >> 8)) & 3;
-    uint32_t bq = 20 + ((((uint32_t)(hr >> 16) & 0xFFFFu) * 21u) >> 16);
-    uint32_t strand = (uint32_t)((hr >> 40) & 1);
+    // ~0.8 % errors; fixed-point ranges (no division): other base 1..3 steps away, baseQ 20..40
+    if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((((hr >> 8) & 0xFFu) * 3u) >> 8)) & 3;
+    const uint32_t bq = 20 + ((((hr >> 16) & 0xFFFFu) * 21u) >> 16);
+    const uint32_t strand = ((hr >> 8) ^ (hr >> 17)) & 1u;
     return bq | (60u << 8) | ((1u << base) << 16) | (strand << 20);
+}
+// every synthetic read survives call_base's filters: baseQ 20..40 (no Illumina offset), mapQ 60,
+// one-hot A/C/G/T bases
+__host__ __device__ inline bool synth_all_pass(uint32_t min_baseQ, uint32_t min_mapQ, bool illumina) {
+    return !illumina && min_baseQ <= 20u && min_mapQ <= 60u;
 }
 __host__ __device__ inline uint8_t synth_ref_char(const SynthSite &s) { return (uint8_t)"ACGT"[s.ref_idx]; }
 

@@ -152,6 +152,14 @@ class HotPath:
         self.n_win = len(windows)
         p = ctx.params
         self.out = WindowOutputs(self.n_win, p.n_samples, p.n_pops, device, ctx.sfs_stride)
+        fields = self.fields_for(stats)
+        self.out_struct = self.out.struct(fields)
+        self.opts = _lib.PbgStatOpts(stats, min_freq, 0, 0)
+        self.pl = synth.pileup()
+
+    @staticmethod
+    def fields_for(stats: int) -> list[str]:
+        """pbg_window_out fields a statistics mask writes."""
         fields = ["num_sites", "segsites"]
         if stats & _lib.PBG_S_NUCDIV:
             fields += ["pi", "dxy"]
@@ -167,9 +175,7 @@ class HotPath:
             fields += ["nhaps", "hap_val", "hap_dxy", "hap_min"]
         if stats & _lib.PBG_S_TREE:
             fields += ["tree_diff"]
-        self.out_struct = self.out.struct(fields)
-        self.opts = _lib.PbgStatOpts(stats, min_freq, 0, 0)
-        self.pl = synth.pileup()
+        return fields
 
     def call(self, stream=None, cb: torch.Tensor | None = None):
         s = stream_handle(stream)

@@ -1,0 +1,71 @@
+"""Whole-genome pass (popbam_amd.genome, configs[3]): the contig-first shard plan covers every
+window exactly once, and the chunked, double-buffered pass -- pileup generated chunk by chunk
+on one stream, called on another, rows kept genome-resident -- gives the same rows and the same
+window statistics, byte for byte, as one batch per contig."""
+import numpy as np
+import pytest
+
+from popbam_amd import genome, workload
+
+SEED = 0xC0FFEE04
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8, 16, 30])
+@pytest.mark.parametrize("lengths,win", [([125_000_000] * 24, 10_000), ([30_017, 1_000_000, 64, 250_001], 1_000),
+                                         ([5_000_000], 10_000), ([999, 10_001, 20_000], 1_000)])
+def test_plan_covers_every_window_once(world, lengths, win):
+    plan = genome.plan_genome(lengths, world, win)
+    assert len(plan) == world
+    got = {}
+    for segs in plan:
+        for s in segs:
+            for a, b in genome.contig_windows(s.end, win, s.beg, s.end):
+                key = (s.contig, a, b)
+                assert key not in got
+                got[key] = True
+            assert 0 <= s.beg < s.end <= lengths[s.contig]
+    want = {(ci, a, b) for ci, L in enumerate(lengths) for a, b in genome.contig_windows(L, win)}
+    assert set(got) == want
+    loads = [sum(s.end - s.beg for s in segs) for segs in plan]
+    if world <= len(lengths):
+        assert max(loads) <= 2 * (sum(lengths) / world) + max(win, max(lengths) // world + win)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,npops", [(12, 2), (24, 2)])
+def test_chunked_pass_equals_one_batch(gpu_lib, n, npops):
+    import torch
+    from popbam_amd import _lib
+    ctx = _lib.Context(workload.default_params(n, npops), 0)
+    lengths = [640_017, 1_000_000, 300_000]
+    segs = [genome.Segment(i, 0, L) for i, L in enumerate(lengths)] + [genome.Segment(1, 250_000, 700_001)]
+    stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS | _lib.PBG_S_DIV_IND
+    small = genome.GenomePass(ctx, segs, SEED, 10, 10_000, stats, chunk=64 * 2000)
+    small.run()
+    small.run()   # a second pass over the same buffers gives the same result
+    small.synchronize()
+    big = genome.GenomePass(ctx, segs, SEED, 10, 10_000, stats, chunk=64 * 20000)
+    big.run()
+    big.synchronize()
+    assert len(small.chunks) > len(big.chunks)
+    for si, s in enumerate(segs):
+        a = small.segment_rows(si).cpu().numpy()
+        b = big.segment_rows(si).cpu().numpy()
+        assert np.array_equal(a, b), si
+        # one batch of the segment through the plain hot path
+        syn = workload.SynthPileup(ctx, s.end - s.beg, 10, SEED, contig=s.contig, pos0=s.beg)
+        wins = [(x - s.beg, y - s.beg) for x, y in genome.contig_windows(s.end, 10_000, s.beg, s.end)]
+        hp = workload.HotPath(ctx, syn, wins or [(0, 0)], stats)
+        hp.step()
+        ctx.sync_check()
+        assert np.array_equal(hp.rows.cpu().numpy(), a), si
+    for f in workload.HotPath.fields_for(stats):
+        x, y = small.window_results(f), big.window_results(f)
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), f
+    # the window outputs of the last segment against its one-batch hot path
+    nw = len(wins)
+    for f in ("pi", "td", "ld_val", "div_ind", "theta_w", "sfs_bins"):
+        per = hp.out.t[f].numel() // max(1, len(wins))
+        tail = small.window_results(f)[-nw * per:]
+        assert np.array_equal(tail.view(np.uint8), hp.out.t[f][:nw * per].cpu().numpy().view(np.uint8)), f
+    ctx.close()
