@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--depth", type=int, default=10)
     ap.add_argument("--window", type=int, default=10_000)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xC0FFEE02)
-    ap.add_argument("--cpu-sample", type=int, default=60_000, help="positions for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=60_000, help="positions for the CPU port baseline (0 = skip all)")
+    ap.add_argument("--ref-sample", type=int, default=200_000, help="positions for the reference-binary baseline")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3),
                     help="BASELINE.json configs[i]: 2 = 50 Msites x 12 samples (the metric's config), "
                          "3 = whole genome 24 contigs x 125 Mbp x 24 samples, nucdiv+sfs+ld+diverge")
@@ -59,10 +60,10 @@ def parse():
     return args
 
 
-def cpu_baseline(args):
+def cpu_port(args):
     """Oracle (kind 'port', 1 core): three separate runs -- nucdiv, sfs, ld -- as the
     reference computes them, each re-calling every position, over the first --cpu-sample
-    positions of the same synthetic pileup."""
+    positions of the same synthetic pileup (no BAM decoding or pileup)."""
     import numpy as np
 
     import harness
@@ -96,6 +97,32 @@ def cpu_baseline(args):
             "sample": f"first {L} positions of the same synthetic pileup ({n} samples, depth {args.depth}); "
                       f"oracle C++ restatement, nucdiv+sfs+ld as 3 separate passes (each re-calls all sites), "
                       f"{win} bp windows; excludes BAM decode/pileup"}
+
+
+def cpu_baseline(args):
+    """POPBAM itself (oracle/_ref/popbam, built from /root/reference) on a BAM of the same
+    synthetic genome (tests/ref_baseline.py): nucdiv, sfs and ld as three processes, wall times
+    summed, on the first --ref-sample positions; plus P region-sharded processes per command
+    (P = the host's CPU share, at most 16).  The oracle port's rate is reported beside it."""
+    import ref_baseline
+    port = cpu_port(args)
+    if not ref_baseline.available():
+        return port
+    L, n = args.ref_sample, args.samples
+    d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_{args.seed:x}_{L}_{n}", args.seed, L, n)
+    procs = max(1, min(16, os.cpu_count() or 1))
+    t = ref_baseline.time_reference(d, L, args.window, procs)
+    out = {"value": round(L / t["single_total_s"] / 1e6, 6), "unit": "Msites/s", "cores": 1, "kind": "reference",
+           "sample": f"oracle/_ref/popbam (POPBAM 0.3 built from /root/reference) nucdiv, sfs, ld -w "
+                     f"{args.window // 1000} as 3 processes (wall {t['single_total_s']:.2f} s summed) on a BAM of "
+                     f"positions [0, {L}) of the same synthetic genome: {n} samples, 100 bp reads every 10 bp "
+                     f"(depth 10), baseQ 40, mapQ 60, 2 populations; includes BAM decode + pileup",
+           "port": port}
+    if "parallel_total_s" in t:
+        out["all_cores"] = {"value": round(L / t["parallel_total_s"] / 1e6, 6), "cores": t["procs"],
+                            "sample": f"{t['procs']} region-sharded processes per command, concurrent "
+                                      f"(wall {t['parallel_total_s']:.2f} s summed over the 3 commands)"}
+    return out
 
 
 def bench_genome(args, torch, dist, world, rank):

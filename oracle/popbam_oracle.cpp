@@ -1204,3 +1204,26 @@ extern "C" uint64_t orc_synth_batch(uint64_t seed, int32_t contig, uint64_t pos_
     }
     return off;
 }
+
+// The genotypes behind the synthetic pileup: per position the reference base, per (position,
+// sample) the two haplotype alleles a0 | a1 << 2 that synth_read draws from (test-only: the CPU
+// baseline writes a BAM of 100 bp reads from them for the reference binary).
+extern "C" void orc_synth_genotypes(uint64_t seed, int32_t contig, uint64_t pos_lo, uint32_t L, int32_t n,
+                                    uint8_t *ref, uint8_t *alleles) {
+    for (uint32_t i = 0; i < L; ++i) {
+        const uint64_t pos = pos_lo + i;
+        uint64_t h = sm64(seed ^ sm64(pos ^ ((uint64_t)(uint32_t)contig << 40)));
+        int ref_idx = (int)(h & 3);
+        int snp = ((h >> 2) & 0x3FF) < 12;
+        int alt = (ref_idx + 1 + (int)((((h >> 12) & 0xFFFFu) * 3u) >> 16)) & 3;
+        uint32_t f16 = (uint32_t)((h >> 16) & 0xFFFF);
+        ref[i] = (uint8_t)"ACGT"[ref_idx];
+        for (int s = 0; s < n; ++s) {
+            uint64_t hs = sm64(h ^ (0xD1B54A32D192ED03ULL * (uint64_t)(s + 1)));
+            int a0 = (snp && (uint32_t)(hs & 0xFFFF) < f16) ? alt : ref_idx;
+            int a1 = (snp && (uint32_t)((hs >> 16) & 0xFFFF) < f16) ? alt : ref_idx;
+            alleles[(size_t)i * n + s] = (uint8_t)(a0 | (a1 << 2));
+        }
+    }
+}
+

@@ -18,6 +18,8 @@ EOF_BLOCK = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000
 
 CIGAR_OPS = "MIDNSHP=X"
 SEQ_NT16 = {c: i for i, c in enumerate("=ACMGRSVTWYHKDBN")}
+# byte -> 4-bit code (upper-cased; anything else -> N = 15), for bytes.translate
+_NT16_TR = bytes(SEQ_NT16.get(chr(b).upper(), 15) for b in range(256))
 
 
 def reg2bin(beg: int, end: int) -> int:
@@ -62,13 +64,8 @@ class Read:
         ncig = len(self.cigar)
         cig = b"".join(struct.pack("<I", n << 4 | CIGAR_OPS.index(op)) for op, n in self.cigar)
         lseq = len(self.seq)
-        packed = bytearray((lseq + 1) // 2)
-        for i, c in enumerate(self.seq):
-            v = SEQ_NT16.get(c.upper(), 15)
-            if i & 1:
-                packed[i >> 1] |= v
-            else:
-                packed[i >> 1] |= v << 4
+        codes = self.seq.encode("latin-1").translate(_NT16_TR) + (b"\0" if lseq & 1 else b"")
+        packed = bytes((codes[i] << 4) | codes[i + 1] for i in range(0, len(codes), 2))
         qual = bytes(self.qual) if lseq else b""
         aux = b"".join(k.encode() + b"Z" + str(v).encode() + b"\0" for k, v in self.tags.items())
         bin_ = reg2bin(self.pos, self.end)
