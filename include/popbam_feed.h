@@ -88,14 +88,17 @@ int  pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refse
                 int n_samples, int max_depth, pbf_batch *out);
 void pbf_batch_free(pbf_batch *batch);
 
-/* pbf_pileup over [beg, end) split into `chunk`-position pieces (rounded up to a multiple of
- * 64; <= 0 = 1 Mb) walked by `n_threads` threads, each with its own handle on `bam_path`.
- * A position's pileup depends only on the reads overlapping it, and bam_fetch of a piece
- * returns all of them in file order, so the merged batch equals one pbf_pileup over the whole
- * range (the host walk multithreaded by region).  On failure the error is the
- * one of the first failing piece in position order.                                      */
+/* The pileup the reference's window loop sees over [beg, end), split into `chunk`-position
+ * pieces (rounded up to a multiple of 64; <= 0 = 1 Mb) walked by `n_threads` threads, each
+ * with its own handle on `bam_path` (the host walk multithreaded by region).
+ * The reference fetches and walks every window on its own (pop_nucdiv.cpp:57-125): window k
+ * of win_size > 0 is [beg + k*win_size, beg + (k+1)*win_size - 1); win_size = 0 means one walk
+ * of [beg, end).  A position's pileup depends only on the reads overlapping it unless a
+ * read meets a full buffer (maxcnt 8000, bam_pileup.c:375), so a piece where no read can is
+ * walked once; a piece where one can is walked window by window as the reference does.
+ * On failure the error is the one of the first failing piece in position order.          */
 int  pbf_pileup_mt(const char *bam_path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
-                   const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
+                   int32_t win_size, const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
                    int32_t fallback_sample, int n_samples, int max_depth, pbf_batch *out);
 
 /* call_base's per-read loop (popbam.cpp:252-287) over a raw batch: keeps a read iff
@@ -107,7 +110,7 @@ void pbf_keys_free(pbf_keys *keys);
 /* pbf_pileup_mt + pbf_pack: each thread packs its own pieces, so the raw reads of the whole
  * region are never held at once.  Same batch as pbf_pack(pbf_pileup_mt(...)).            */
 int  pbf_pileup_keys_mt(const char *bam_path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
-                        const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
+                        int32_t win_size, const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
                         int32_t fallback_sample, int n_samples, int max_depth, const pbf_filter *f,
                         pbf_keys *out);
 

@@ -1082,7 +1082,7 @@ long orc_run(const orc_params *p, const orc_cmd *c, uint32_t n_sites, const uint
     SfsConst K = sfs_const(n);
     Out o;
     Window W;
-    if (c->cmd == ORC_SNP && c->output == 2) ms_header(o, p, num_windows);
+    if (c->cmd == ORC_SNP && c->output == 2 && num_windows > 0) ms_header(o, p, num_windows);   // cw == 0 only
     for (long cw = 0; cw < num_windows; cw++) {
         int wb, we;
         if (c->windowed) {  // "chr:beg+cw*w+1-(cw+1)*w+beg-1" through bam_parse_region

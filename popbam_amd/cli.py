@@ -9,6 +9,8 @@ subcommands snp, nucdiv, sfs, ld, diverge, haplo and tree:
   -> per block of whole windows: pileup + per-sample partition + call_base's per-read loop
      (libpopbam_feed.so, multithreaded; the next block is read while the GPU runs this one)
   -> pbg_run (libpopbam_gpu.so: consensus call, the reference's window loop, print_<cmd>).
+Multi-GPU: POPBAM_WORLD=N (or a torchrun launch) splits the window list into N contiguous
+blocks, one rank process per GPU (popbam_amd.shard); rank 0 prints the blocks in order.
 Blocks bound host and device memory by the block, not the region (the reference re-fetches
 every window, pop_nucdiv.cpp:57-125); the text is the concatenation of the blocks' texts.
 stdout is the reference's TSV byte for byte; errors are reported like fatal_error
@@ -56,8 +58,10 @@ def window_blocks(beg: int, end: int, win_size: int, windowed: bool, block_sites
     return [(beg + a * win_size, beg + min(nw, a + per) * win_size + 1) for a in range(0, nw, per)]
 
 
-def run(cmd: str, argv: list[str], device: int = 0) -> str:
-    """One `popbam <cmd> argv...` invocation; returns stdout text (raises PopbamError)."""
+def run(cmd: str, argv: list[str], device: int = 0, rank: int = 0, world: int = 1) -> str:
+    """One `popbam <cmd> argv...` invocation; returns stdout text (raises PopbamError).
+    With world > 1 this rank computes only its block of windows (popbam_amd.shard) and
+    returns that block's text; the blocks concatenated in rank order are the full output."""
     from concurrent.futures import ThreadPoolExecutor
 
     from . import _lib, engine, feed, shard
@@ -89,8 +93,14 @@ def run(cmd: str, argv: list[str], device: int = 0) -> str:
         fallback = 0 if not sm.rg2sample else -1
         windowed = bool(o.flag & opt.BAM_WINDOW)
         threads = int(os.environ.get("POPBAM_FEED_THREADS", min(8, os.cpu_count() or 1)))
-        blocks = [b for b in window_blocks(beg, end, o.win_size, windowed,
-                                           int(os.environ.get("POPBAM_BLOCK_SITES", 1 << 22)))]
+        nw_total = shard.num_windows(beg, end, o.win_size, windowed)
+        rbeg, rend, ms0 = beg, end, nw_total
+        if world > 1:
+            reg = shard.shard_region(beg, end, o.win_size, windowed, rank, world)
+            if reg is None:
+                return ""
+            (rbeg, rend), ms0 = reg, shard.ms_windows_for(beg, end, o.win_size, windowed, rank)
+        blocks = window_blocks(rbeg, rend, o.win_size, windowed, int(os.environ.get("POPBAM_BLOCK_SITES", 1 << 22)))
         flt = engine.make_filter(o)
 
         def pile(reg):
@@ -98,13 +108,12 @@ def run(cmd: str, argv: list[str], device: int = 0) -> str:
             chunk = max(1 << 16, -(-(hi - lo) // max(1, 4 * threads)))
             try:
                 return lo, bam.pileup_keys(tid, lo, hi, seq, sm.rg2sample, sm.n, o.max_depth, flt, fallback,
-                                           threads=threads, chunk=chunk)
+                                           threads=threads, chunk=chunk, win=o.win_size if windowed else 0)
             except feed.FeedError as e:
                 if e.code == feed.PBF_E_RG:
                     raise opt.PopbamError("Problem assigning read group") from e
                 raise opt.PopbamError(f"Failed to retrieve region {o.region}: {e}") from e
 
-        nw_total = shard.num_windows(beg, end, o.win_size, windowed)
         if not blocks:   # no window: the reference's loop prints nothing
             return ""
         ctx = _lib.Context(engine.make_params(o, sm), device)
@@ -116,7 +125,7 @@ def run(cmd: str, argv: list[str], device: int = 0) -> str:
                     lo, batch = nxt.result()
                     if i + 1 < len(blocks):
                         nxt = ex.submit(pile, blocks[i + 1])
-                    ms = (nw_total if i == 0 else -1) if len(blocks) > 1 else 0
+                    ms = (ms0 if i == 0 else -1) if len(blocks) > 1 or world > 1 else 0
                     parts.append(engine.run_command(o, sm, names[tid], reg[0], reg[1], batch, pos0=lo, ctx=ctx,
                                                     refid=refid, ms_windows=ms))
                     del batch
@@ -125,6 +134,61 @@ def run(cmd: str, argv: list[str], device: int = 0) -> str:
         return "".join(parts)
     finally:
         bam.close()
+
+
+def _run_rank(cmd: str, argv: list[str]) -> int:
+    """One rank of a sharded run (launched by _launch_ranks or torchrun): compute this rank's
+    windows on GPU LOCAL_RANK, gather (status, text) to rank 0 over gloo, rank 0 prints.
+    Every rank reaches the gather, also after an error, so a failing rank cannot hang the rest."""
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    # the gloo runtime logs to file descriptor 1; keep stdout for the reference's TSV only
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        try:
+            import torch
+            ndev = max(1, torch.cuda.device_count())
+            dev = int(os.environ.get("POPBAM_DEVICE", int(os.environ.get("LOCAL_RANK", rank)) % ndev))
+            res = (0, run(cmd, argv, device=dev, rank=rank, world=world))
+        except opt.PopbamError as e:
+            res = (1, str(e))
+        parts = [None] * world if rank == 0 else None
+        dist.gather_object(res, parts, dst=0)
+    finally:
+        dist.destroy_process_group()
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+    if rank != 0:
+        return res[0]
+    for code, msg in parts:
+        if code:
+            return _fatal(msg)
+    sys.stdout.write("".join(t for _, t in parts))
+    sys.stdout.flush()
+    return 0
+
+
+def _launch_ranks(world: int, argv: list[str]) -> int:
+    """POPBAM_WORLD=N: start N rank processes of this command (one per GPU, round-robin over the
+    visible GPUs), rank 0's stdout is the command's stdout.  The launcher itself never touches
+    the GPU; it starts children and returns the first non-zero status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), POPBAM_WORLD="1",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-m", "popbam_amd.cli", *argv], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    codes = [p.wait() for p in procs]
+    return next((c for c in codes if c), 0)
 
 
 def main(argv: list[str] | None = None) -> int:
@@ -136,6 +200,12 @@ def main(argv: list[str] | None = None) -> int:
     if cmd not in COMMANDS:
         sys.stderr.write(f"Error: unrecognized command: {cmd}\n")
         return 1
+    # multi-GPU: POPBAM_WORLD=N starts N ranks; a torchrun launch (WORLD_SIZE > 1) is one rank
+    world = int(os.environ.get("POPBAM_WORLD", "1"))
+    if world > 1:
+        return _launch_ranks(world, argv)
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return _run_rank(cmd, argv[1:])
     try:
         text = run(cmd, argv[1:], device=int(os.environ.get("POPBAM_DEVICE", "0")))
     except opt.PopbamError as e:

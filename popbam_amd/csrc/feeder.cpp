@@ -443,62 +443,60 @@ void pbf_batch_free(pbf_batch *o) {
 
 void pbf_free(void *p) { free(p); }
 
-int pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refseq, const char *const *rg_ids,
-               const int32_t *rg_sample, int n_rg, int32_t fallback, int ns, int max_depth, pbf_batch *out) {
-    if (!b || !out || !refseq || ns < 1 || end < beg || tid < 0 || tid >= (int)b->names.size())
-        return fail(PBF_E_ARG, "bad argument");
-    memset(out, 0, sizeof(*out));
-    const uint32_t L = (uint32_t)(end - beg);
-    out->n_sites = L;
-    out->pos0 = beg;
-    out->ref = (uint8_t *)malloc(std::max<size_t>(L, 1));
-    out->depth = (uint16_t *)calloc(std::max<size_t>((size_t)L * ns, 1), sizeof(uint16_t));
-    out->block_off = (uint64_t *)calloc(L / 64 + 2, sizeof(uint64_t));
-    if (!out->ref || !out->depth || !out->block_off) {
-        pbf_batch_free(out);
-        return fail(PBF_E_IO, "out of host memory");
-    }
-    for (uint32_t i = 0; i < L; ++i) out->ref[i] = (uint8_t)refseq[beg + i] | 0x80;
-    std::unordered_map<std::string, int32_t> rgmap;
-    for (int i = 0; i < n_rg; ++i) rgmap[rg_ids[i]] = rg_sample[i];
+}  // extern "C"
 
-    // bam_fetch: reads overlapping [beg, end) in file order
-    std::vector<Rec> recs;
+namespace {
+
+// bam_fetch: reads of `tid` overlapping [lo, hi) in file order (bam_index.c:884-980)
+int fetch_region(pbf_bam *b, int tid, int32_t lo, int32_t hi, std::vector<Rec> &recs) {
+    recs.clear();
     uint64_t start;
-    if (L > 0 && region_start(b, tid, beg, end, start)) {
-        int r = b->z.seek(start);
-        if (r < 0) {
-            pbf_batch_free(out);
-            return r;
+    if (hi <= lo || !region_start(b, tid, lo, hi, start)) return PBF_OK;
+    int r = b->z.seek(start);
+    if (r < 0) return r;
+    Rec rec;
+    while ((r = read_rec(b->z, rec)) == 1) {
+        if (rec.tid != tid) {
+            if (b->has_index || (rec.tid > tid)) break;   // sorted: past the contig
+            continue;
         }
-        Rec rec;
-        while ((r = read_rec(b->z, rec)) == 1) {
-            if (rec.tid != tid) {
-                if (b->has_index || (rec.tid > tid)) break;   // sorted: past the contig
-                continue;
-            }
-            if (rec.pos >= end) break;
-            const int32_t oend = rec.cigar.empty() ? rec.pos + 1 : rec.end;
-            if (oend > beg && rec.pos < end) recs.push_back(rec);
-        }
-        if (r < 0) {
-            pbf_batch_free(out);
-            return r;
-        }
+        if (rec.pos >= hi) break;
+        const int32_t oend = rec.cigar.empty() ? rec.pos + 1 : rec.end;
+        if (oend > lo && rec.pos < hi) recs.push_back(rec);
     }
+    return r < 0 ? r : PBF_OK;
+}
 
-    // pileup walk (bam_plp_push / bam_plp_next), restricted to [beg, end) for the output
-    std::vector<Node> buf;            // push order
-    std::vector<std::vector<uint32_t>> per(ns);
+constexpr int kMaxCnt = 8000;                               // bam_plp maxcnt (bam_pileup.c:375)
+constexpr uint16_t kDefMask = 0x4 | 0x100 | 0x200 | 0x400;   // BAM_DEF_MASK (bam.h:123)
+
+struct WalkCfg {
+    std::unordered_map<std::string, int32_t> rgmap;
+    int32_t fallback;
+    int ns, max_depth;
+};
+
+// positions [p0, p0 + n) of a batch, filled in position order by one or more walks
+struct WalkOut {
+    int32_t p0;
+    uint32_t n;
+    uint8_t *ref;
+    uint16_t *depth;
     std::vector<uint32_t> reads;
-    reads.reserve(recs.size() * 64);
+};
+
+// One bam_plp walk (bam_plp_push / bam_plp_next) over `recs`; positions in [ebeg, eend) get
+// the callback's per-sample partition (popbam.cpp:220-249) written into `o`.  Walks that fill
+// one batch must come in increasing, disjoint [ebeg, eend).
+int walk(const std::vector<Rec> &recs, int32_t ebeg, int32_t eend, const WalkCfg &cf, WalkOut &o) {
+    std::vector<Node> buf;            // push order
+    std::vector<std::vector<uint32_t>> per(cf.ns);
     int32_t ipos = 0, itid = 0, max_pos = -1, max_tid = -1;
-    const uint16_t kMask = 0x4 | 0x100 | 0x200 | 0x400;   // BAM_DEF_MASK
     int err = 0;
-    auto emit = [&](int32_t pos) {   // one callback: partition + copy (popbam.cpp:220-249)
-        if (pos < beg || pos >= end) return;
-        const uint32_t i = (uint32_t)(pos - beg);
-        out->ref[i] &= 0x7F;
+    auto emit = [&](int32_t pos) {
+        if (pos < ebeg || pos >= eend) return;
+        const uint32_t i = (uint32_t)(pos - o.p0);
+        o.ref[i] &= 0x7F;
         for (auto &v : per) v.clear();
         for (Node &n : buf) {
             if (n.r->pos > pos || n.r->end <= pos) continue;
@@ -506,24 +504,22 @@ int pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refseq
             const int kind = resolve(n, pos, &qp);
             if (kind != 0 || (n.r->flag & 0x4)) continue;
             if (!n.r->has_rg) continue;
-            int32_t s;
-            auto it = rgmap.find(n.r->rg);
-            s = it != rgmap.end() ? it->second : fallback;
-            if (s < 0 || s >= ns) {
+            auto it = cf.rgmap.find(n.r->rg);
+            const int32_t s = it != cf.rgmap.end() ? it->second : cf.fallback;
+            if (s < 0 || s >= cf.ns) {
                 if (!err) err = fail(PBF_E_RG, "Problem assigning read group " + n.r->rg +
                                                    " to a sample.\nPlease check BAM header for correct SM and PO tags");
                 continue;
             }
-            if ((int)per[s].size() >= max_depth) continue;
+            if ((int)per[s].size() >= cf.max_depth) continue;
             const uint32_t strand = (n.r->flag >> 4) & 1u;
             per[s].push_back((uint32_t)n.r->qual[qp] | (uint32_t)n.r->mapq << 8 | (uint32_t)n.r->nt16[qp] << 16 |
                              strand << 20);
         }
-        for (int s = 0; s < ns; ++s) {
-            out->depth[(size_t)i * ns + s] = (uint16_t)per[s].size();
-            reads.insert(reads.end(), per[s].begin(), per[s].end());
+        for (int s = 0; s < cf.ns; ++s) {
+            o.depth[(size_t)i * cf.ns + s] = (uint16_t)per[s].size();
+            o.reads.insert(o.reads.end(), per[s].begin(), per[s].end());
         }
-        // block offsets are prefix sums over positions; positions are emitted in order
     };
     // emits every pending position below max_pos (or all at EOF), dropping finished reads
     auto next = [&](bool eof) {
@@ -556,8 +552,8 @@ int pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refseq
         }
     };
     for (const Rec &r : recs) {
-        if (r.tid < 0 || (r.flag & kMask)) continue;
-        if (itid == r.tid && ipos == r.pos && (int)buf.size() + 2 > 8000) continue;   // maxcnt
+        if (r.tid < 0 || (r.flag & kDefMask)) continue;
+        if (itid == r.tid && ipos == r.pos && (int)buf.size() + 2 > kMaxCnt) continue;   // maxcnt
         max_tid = r.tid;
         max_pos = r.pos;
         if (r.end > ipos || r.tid > itid) {
@@ -568,11 +564,99 @@ int pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refseq
         next(false);
     }
     next(true);
-    if (err) {
-        pbf_batch_free(out);
-        return err;
+    return err;
+}
+
+// Upper bound of the pileup buffer at each maxcnt test: a read starting at p meets at most
+// the unmasked reads before it that still reach p (the walk drops a read only after passing
+// its end).  Returns the largest bound over the reads that matter for positions >= from
+// (reads starting there, or reaching it).
+int max_buffer_bound(const std::vector<Rec> &a, int32_t from) {
+    std::vector<int32_t> ends;   // min-heap of the ends of earlier reads
+    int best = 0;
+    for (const Rec &r : a) {
+        if (r.tid < 0 || (r.flag & kDefMask)) continue;
+        while (!ends.empty() && ends.front() < r.pos) {
+            std::pop_heap(ends.begin(), ends.end(), std::greater<int32_t>());
+            ends.pop_back();
+        }
+        if (r.pos >= from || r.end >= from) best = std::max(best, (int)ends.size());
+        ends.push_back(std::max(r.end, r.pos + 1));
+        std::push_heap(ends.begin(), ends.end(), std::greater<int32_t>());
     }
-    // per-64-position read offsets
+    return best;
+}
+
+// Positions [cb, ce) of a region [rbeg, rend) that the reference walks window by window
+// (win > 0: window k is [rbeg + k*win, rbeg + (k+1)*win - 1), a fresh bam_fetch + pileup per
+// window, pop_nucdiv.cpp:57-125; win == 0: one walk of the whole region).
+// When no read that reaches [cb, ce) can meet a full buffer (max_buffer_bound + 2 <= maxcnt),
+// every walk keeps every read, so one walk of the reads overlapping [cb, ce) gives the
+// reference's pileup there.  Otherwise the maxcnt drops depend on where the reference's walk
+// started: walk each window of the reference (and each position between windows) on its own.
+int chunk_walk(pbf_bam *b, int tid, int32_t cb, int32_t ce, int32_t rbeg, int32_t rend, int32_t win,
+               const WalkCfg &cf, WalkOut &o) {
+    std::vector<Rec> recs, early;
+    int r = fetch_region(b, tid, std::max(0, cb - 1), ce, recs);
+    if (r != PBF_OK) return r;
+    int32_t lo = cb;
+    for (const Rec &x : recs)
+        if (!(x.flag & kDefMask)) lo = std::min(lo, x.pos);
+    int bound;
+    if (lo < cb) {   // the reads before cb that reach it: their tests see reads ending before cb too
+        r = fetch_region(b, tid, std::max(0, lo - 1), cb, early);
+        if (r != PBF_OK) return r;
+        std::vector<Rec> all;
+        for (const Rec &x : early)
+            if (x.pos < cb) all.push_back(x);
+        for (const Rec &x : recs)
+            if (x.pos >= cb) all.push_back(x);
+        bound = max_buffer_bound(all, cb);
+    } else {
+        bound = max_buffer_bound(recs, cb);
+    }
+    if (bound + 2 <= kMaxCnt) return walk(recs, cb, ce, cf, o);
+    // crowded: the reference's own walks
+    int32_t a = cb;
+    while (a < ce) {
+        int32_t sa, sb;   // the reference walk that covers position a
+        if (win <= 0) {
+            sa = rbeg, sb = rend;
+        } else {
+            const int64_t k = ((int64_t)a - rbeg) / win;
+            const int64_t wb = rbeg + k * win, we = wb + win - 1;
+            if (a < we) sa = (int32_t)wb, sb = (int32_t)std::min<int64_t>(we, rend);
+            else sa = a, sb = a + 1;   // the last base of a window: in no window
+        }
+        sb = std::max(sb, a + 1);
+        r = fetch_region(b, tid, sa, sb, recs);
+        if (r != PBF_OK) return r;
+        const int32_t e = std::min(sb, ce);
+        r = walk(recs, a, e, cf, o);
+        if (r != PBF_OK) return r;
+        a = e;
+    }
+    return PBF_OK;
+}
+
+int batch_alloc(pbf_batch *out, int32_t beg, uint32_t L, int ns, const char *refseq) {
+    memset(out, 0, sizeof(*out));
+    out->n_sites = L;
+    out->pos0 = beg;
+    out->ref = (uint8_t *)malloc(std::max<size_t>(L, 1));
+    out->depth = (uint16_t *)calloc(std::max<size_t>((size_t)L * ns, 1), sizeof(uint16_t));
+    out->block_off = (uint64_t *)calloc(L / 64 + 2, sizeof(uint64_t));
+    if (!out->ref || !out->depth || !out->block_off) {
+        pbf_batch_free(out);
+        return fail(PBF_E_IO, "out of host memory");
+    }
+    for (uint32_t i = 0; i < L; ++i) out->ref[i] = (uint8_t)refseq[beg + i] | 0x80;
+    return PBF_OK;
+}
+
+// block offsets + reads of a filled batch
+int batch_finish(pbf_batch *out, int ns, std::vector<uint32_t> &reads) {
+    const uint32_t L = out->n_sites;
     uint64_t acc = 0;
     for (uint32_t bk = 0; bk * 64 < L; ++bk) {
         out->block_off[bk] = acc;
@@ -591,11 +675,59 @@ int pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refseq
     return PBF_OK;
 }
 
-int pbf_pileup_mt(const char *path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
+WalkCfg make_cfg(const char *const *rg_ids, const int32_t *rg_sample, int n_rg, int32_t fallback, int ns,
+                 int max_depth) {
+    WalkCfg cf;
+    for (int i = 0; i < n_rg; ++i) cf.rgmap[rg_ids[i]] = rg_sample[i];
+    cf.fallback = fallback;
+    cf.ns = ns;
+    cf.max_depth = max_depth;
+    return cf;
+}
+
+// one piece [cb, ce) of a region as a raw batch
+int piece_batch(pbf_bam *b, int tid, int32_t cb, int32_t ce, int32_t rbeg, int32_t rend, int32_t win,
+                const char *refseq, const WalkCfg &cf, pbf_batch *out) {
+    int r = batch_alloc(out, cb, (uint32_t)(ce - cb), cf.ns, refseq);
+    if (r != PBF_OK) return r;
+    WalkOut o{cb, (uint32_t)(ce - cb), out->ref, out->depth, {}};
+    r = chunk_walk(b, tid, cb, ce, rbeg, rend, win, cf, o);
+    if (r != PBF_OK) {
+        pbf_batch_free(out);
+        return r;
+    }
+    return batch_finish(out, cf.ns, o.reads);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pbf_pileup(pbf_bam *b, int tid, int32_t beg, int32_t end, const char *refseq, const char *const *rg_ids,
+               const int32_t *rg_sample, int n_rg, int32_t fallback, int ns, int max_depth, pbf_batch *out) {
+    if (!b || !out || !refseq || ns < 1 || end < beg || tid < 0 || tid >= (int)b->names.size())
+        return fail(PBF_E_ARG, "bad argument");
+    const WalkCfg cf = make_cfg(rg_ids, rg_sample, n_rg, fallback, ns, max_depth);
+    int r = batch_alloc(out, beg, (uint32_t)(end - beg), ns, refseq);
+    if (r != PBF_OK) return r;
+    std::vector<Rec> recs;
+    WalkOut o{beg, (uint32_t)(end - beg), out->ref, out->depth, {}};
+    r = fetch_region(b, tid, beg, end, recs);   // one bam_fetch + pileup of the region
+    if (r == PBF_OK) r = walk(recs, beg, end, cf, o);
+    if (r != PBF_OK) {
+        pbf_batch_free(out);
+        return r;
+    }
+    return batch_finish(out, ns, o.reads);
+}
+
+int pbf_pileup_mt(const char *path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end, int32_t win_size,
                   const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
                   int32_t fallback, int ns, int max_depth, pbf_batch *out) {
-    if (!path || !out || !refseq || ns < 1 || end < beg || n_threads < 1) return fail(PBF_E_ARG, "bad argument");
+    if (!path || !out || !refseq || ns < 1 || end < beg || n_threads < 1 || tid < 0)
+        return fail(PBF_E_ARG, "bad argument");
     memset(out, 0, sizeof(*out));
+    const WalkCfg cf = make_cfg(rg_ids, rg_sample, n_rg, fallback, ns, max_depth);
     const int64_t L = (int64_t)end - beg;
     if (chunk <= 0) chunk = 1 << 20;
     chunk = (chunk + 63) / 64 * 64;   // chunk borders on 64-position blocks: block_off concatenates
@@ -608,10 +740,11 @@ int pbf_pileup_mt(const char *path, int n_threads, int32_t chunk, int tid, int32
     auto worker = [&](int w) {
         pbf_bam *b = nullptr;
         int r = pbf_open(&b, path);
+        if (r == PBF_OK && tid >= (int)b->names.size()) r = fail(PBF_E_ARG, "bad argument");
         for (int64_t c = w; c < nchunk; c += nt) {
             if (r == PBF_OK) {
                 const int32_t cb = (int32_t)(beg + c * chunk), ce = (int32_t)std::min<int64_t>(end, beg + (c + 1) * chunk);
-                r = pbf_pileup(b, tid, cb, ce, refseq, rg_ids, rg_sample, n_rg, fallback, ns, max_depth, &parts[c]);
+                r = piece_batch(b, tid, cb, ce, beg, end, win_size, refseq, cf, &parts[c]);
             }
             rc[c] = r;
             if (r != PBF_OK) msg[c] = g_err;
@@ -724,10 +857,12 @@ int pbf_pack(const pbf_batch *raw, int ns, const pbf_filter *f, pbf_keys *out) {
 }
 
 int pbf_pileup_keys_mt(const char *path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
-                       const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
+                       int32_t win_size, const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
                        int32_t fallback, int ns, int max_depth, const pbf_filter *f, pbf_keys *out) {
-    if (!path || !out || !refseq || !f || ns < 1 || end < beg || n_threads < 1) return fail(PBF_E_ARG, "bad argument");
+    if (!path || !out || !refseq || !f || ns < 1 || end < beg || n_threads < 1 || tid < 0)
+        return fail(PBF_E_ARG, "bad argument");
     memset(out, 0, sizeof(*out));
+    const WalkCfg cf = make_cfg(rg_ids, rg_sample, n_rg, fallback, ns, max_depth);
     const int64_t L = (int64_t)end - beg;
     if (chunk <= 0) chunk = 1 << 20;
     chunk = (chunk + 63) / 64 * 64;   // chunk borders on 64-position blocks: block_off concatenates
@@ -740,11 +875,12 @@ int pbf_pileup_keys_mt(const char *path, int n_threads, int32_t chunk, int tid, 
     auto worker = [&](int w) {
         pbf_bam *b = nullptr;
         int r = pbf_open(&b, path);
+        if (r == PBF_OK && tid >= (int)b->names.size()) r = fail(PBF_E_ARG, "bad argument");
         for (int64_t c = w; c < nchunk; c += nt) {
             if (r == PBF_OK) {
                 const int32_t cb = (int32_t)(beg + c * chunk), ce = (int32_t)std::min<int64_t>(end, beg + (c + 1) * chunk);
                 pbf_batch raw;
-                r = pbf_pileup(b, tid, cb, ce, refseq, rg_ids, rg_sample, n_rg, fallback, ns, max_depth, &raw);
+                r = piece_batch(b, tid, cb, ce, beg, end, win_size, refseq, cf, &raw);
                 if (r == PBF_OK) {
                     r = pbf_pack(&raw, ns, f, &parts[c]);
                     pbf_batch_free(&raw);

@@ -104,10 +104,11 @@ def run_command_sharded(o: opt.Options, sm: opt.SampleModel, chr_name: str, beg:
     from . import shard
     windowed = bool(o.flag & opt.BAM_WINDOW)
 
-    def block(b, e):
+    def block(b, e, ms):
         lo, hi = shard.positions_needed(b, e, o.win_size, windowed)
         hi = max(hi, lo + 1)
         sub = shard.slice_batch(batch, pos0, lo, hi)
-        return run_command(o, sm, chr_name, b, e, sub, pos0=sub["pos0"], device=device, refid=refid)
+        return run_command(o, sm, chr_name, b, e, sub, pos0=sub["pos0"], device=device, refid=refid,
+                           ms_windows=ms)
 
     return shard.run_sharded(block, beg, end, o.win_size, windowed, group)

@@ -72,14 +72,15 @@ def load():
     lib.pbf_has_index.argtypes = [vp]
     lib.pbf_pileup.argtypes = [vp, C.c_int, C.c_int32, C.c_int32, C.c_char_p, P(C.c_char_p), P(C.c_int32),
                                C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfBatch)]
-    lib.pbf_pileup_mt.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int, C.c_int32, C.c_int32, C.c_char_p,
+    lib.pbf_pileup_mt.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                   P(C.c_char_p), P(C.c_int32), C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfBatch)]
     lib.pbf_batch_free.argtypes = [P(PbfBatch)]
     lib.pbf_batch_free.restype = None
     lib.pbf_pack.argtypes = [P(PbfBatch), C.c_int, P(PbfFilter), P(PbfKeys)]
     lib.pbf_keys_free.argtypes = [P(PbfKeys)]
     lib.pbf_keys_free.restype = None
-    lib.pbf_pileup_keys_mt.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int, C.c_int32, C.c_int32, C.c_char_p,
+    lib.pbf_pileup_keys_mt.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int, C.c_int32, C.c_int32, C.c_int32,
+                                       C.c_char_p,
                                        P(C.c_char_p), P(C.c_int32), C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfFilter),
                                        P(PbfKeys)]
     lib.pbf_fasta_fetch.argtypes = [C.c_char_p, C.c_char_p, P(C.c_void_p), P(C.c_int64)]
@@ -163,9 +164,11 @@ class Bam:
         return bool(self.lib.pbf_has_index(self.h))
 
     def pileup(self, tid: int, beg: int, end: int, refseq: bytes, rg2s: dict, n_samples: int, max_depth: int,
-               fallback_sample: int = -1, threads: int = 1, chunk: int = 1 << 20) -> dict:
-        """Dense pileup batch of [beg, end).  threads > 1: pbf_pileup_mt (chunk-position
-        pieces walked in parallel, each thread with its own file handle; same batch)."""
+               fallback_sample: int = -1, threads: int = 1, chunk: int = 1 << 20, win: int = 0) -> dict:
+        """Dense pileup batch of [beg, end).  threads = 1: one walk of the region (pbf_pileup).
+        threads > 1: pbf_pileup_mt (chunk-position pieces walked in parallel, each thread with
+        its own file handle), the pileup of the reference's walks of windows of `win`
+        positions from beg (win = 0: one walk of the region, the same batch as threads = 1)."""
         ids = list(rg2s)
         rg = (C.c_char_p * max(1, len(ids)))(*[i.encode() for i in ids])
         sm = (C.c_int32 * max(1, len(ids)))(*[rg2s[i] for i in ids])
@@ -173,7 +176,7 @@ class Bam:
             raise FeedError(-3, "reference sequence shorter than the region")
         out = PbfBatch()
         if threads > 1:
-            _check(self.lib, self.lib.pbf_pileup_mt(self.path.encode(), threads, chunk, tid, beg, end, refseq, rg, sm,
+            _check(self.lib, self.lib.pbf_pileup_mt(self.path.encode(), threads, chunk, tid, beg, end, win, refseq, rg, sm,
                                                     len(ids), fallback_sample, n_samples, max_depth, C.byref(out)))
         else:
             _check(self.lib, self.lib.pbf_pileup(self.h, tid, beg, end, refseq, rg, sm, len(ids), fallback_sample,
@@ -189,16 +192,17 @@ class Bam:
         return {"ref": ref, "depth": depth.reshape(L, n_samples), "reads": reads, "block_off": boff, "pos0": beg}
 
     def pileup_keys(self, tid: int, beg: int, end: int, refseq: bytes, rg2s: dict, n_samples: int, max_depth: int,
-                    flt: PbfFilter, fallback_sample: int = -1, threads: int = 1, chunk: int = 1 << 20) -> dict:
+                    flt: PbfFilter, fallback_sample: int = -1, threads: int = 1, chunk: int = 1 << 20,
+                    win: int = 0) -> dict:
         """Key batch of [beg, end) (pbf_pileup_keys_mt): pileup + partition + call_base's
-        per-read loop, pieces walked and packed by `threads` threads."""
+        per-read loop, pieces walked and packed by `threads` threads; `win` as in pileup()."""
         ids = list(rg2s)
         rg = (C.c_char_p * max(1, len(ids)))(*[i.encode() for i in ids])
         sm = (C.c_int32 * max(1, len(ids)))(*[rg2s[i] for i in ids])
         if len(refseq) < end:
             raise FeedError(-3, "reference sequence shorter than the region")
         out = PbfKeys()
-        _check(self.lib, self.lib.pbf_pileup_keys_mt(self.path.encode(), max(1, threads), chunk, tid, beg, end, refseq,
+        _check(self.lib, self.lib.pbf_pileup_keys_mt(self.path.encode(), max(1, threads), chunk, tid, beg, end, win, refseq,
                                                      rg, sm, len(ids), fallback_sample, n_samples, max_depth,
                                                      C.byref(flt), C.byref(out)))
         return _take_keys(self.lib, out, n_samples, flt.k_bytes)

@@ -70,16 +70,23 @@ def slice_batch(batch: dict, pos0: int, lo: int, hi: int) -> dict:
             "reads": np.asarray(batch["reads"])[cum[a]:cum[b]], "pos0": pos0 + a}
 
 
+def ms_windows_for(beg: int, end: int, win_size: int, windowed: bool, rank: int) -> int:
+    """`snp -o 2` header control for this rank's block (pbg_cmd.ms_windows): the reference
+    prints one header, with the whole run's window count, before window 0 (pop_snp.cpp:114-115),
+    so rank 0 prints it with the total and every later block prints none."""
+    return num_windows(beg, end, win_size, windowed) if rank == 0 else -1
+
+
 def run_sharded(run_block, beg: int, end: int, win_size: int, windowed: bool, group=None) -> str | None:
-    """Run this rank's block with run_block(beg', end') -> str and gather the fragments to
-    rank 0 in rank order (returns the full text on rank 0, None elsewhere).  Without an
-    initialised process group this is a single-rank run."""
+    """Run this rank's block with run_block(beg', end', ms_windows) -> str and gather the
+    fragments to rank 0 in rank order (returns the full text on rank 0, None elsewhere).
+    Without an initialised process group this is a single-rank run."""
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
-        return run_block(beg, end)
+        return run_block(beg, end, 0)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     reg = shard_region(beg, end, win_size, windowed, rank, world)
-    text = run_block(*reg) if reg is not None else ""
+    text = run_block(*reg, ms_windows_for(beg, end, win_size, windowed, rank)) if reg is not None else ""
     parts = [None] * world if rank == 0 else None
     dist.gather_object(text, parts, dst=0, group=group)
     return "".join(parts) if rank == 0 else None

@@ -36,6 +36,58 @@ def test_cli_matches_reference(gpu_lib, name, idx):
     assert ok, f"{argv}\n gold: {diff[0]}\n ours: {diff[1]}"
 
 
+SHARD_CASES = [("g13_snpformats", 3), ("g13_snpformats", 5), ("g01_base", 0), ("g15_24s3p", 2), ("g12_regions", 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_cli_rank_blocks_concatenate_to_reference(gpu_lib, world):
+    """cli.run(rank=r, world=W) for every r, concatenated in rank order, is the reference's
+    output (window blocks, snp -o 2 header printed once with the run's total)."""
+    for name, idx in SHARD_CASES:
+        cases = fixtures.load_case(name)["meta"]["cases"]
+        cs = cases[min(idx, len(cases) - 1)]
+        argv = _argv(name, cs)
+        ours = "".join(cli.run(argv[0], argv[1:], rank=r, world=world) for r in range(world))
+        gold = fixtures.golden_text(name, cs["stdout"])
+        oob = None
+        if cs["args"][0] == "snp":
+            oob = harness.snp_oob_cells(harness.oracle_run(harness.Setup(name, cs["args"], cs["region"])))
+        ok, diff = harness.same_output(cs["args"], gold, ours, oob)
+        assert ok, f"{argv} world={world}\n gold: {diff[0]}\n ours: {diff[1]}"
+
+
+@pytest.mark.gpu
+def test_cli_popbam_world_two_processes(gpu_lib):
+    """POPBAM_WORLD=2: two rank processes (both on GPU 0 here), text gathered to rank 0 over gloo."""
+    import subprocess
+    import sys
+    name = "g13_snpformats"
+    cs = [c for c in fixtures.load_case(name)["meta"]["cases"] if c["args"] == ["snp", "-o", "2", "-w", "2"]][0]
+    argv = _argv(name, cs)
+    env = dict(os.environ, POPBAM_WORLD="2")
+    r = subprocess.run([sys.executable, "-m", "popbam_amd.cli", *argv], env=env, capture_output=True, timeout=100,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr.decode()
+    gold = fixtures.golden_text(name, cs["stdout"])
+    oob = harness.snp_oob_cells(harness.oracle_run(harness.Setup(name, cs["args"], cs["region"])))
+    ok, diff = harness.same_output(cs["args"], gold, r.stdout.decode(), oob)
+    assert ok, diff
+
+
+def test_cli_popbam_world_reports_rank_errors(tmp_path):
+    """A sharded run whose ranks fail before the GPU: rank 0 reports the error, status 1, no hang."""
+    import subprocess
+    import sys
+    d = fixtures.load_case("g01_base")["dir"]
+    env = dict(os.environ, POPBAM_WORLD="2")
+    r = subprocess.run([sys.executable, "-m", "popbam_amd.cli", "nucdiv", "-f", os.path.join(d, "ref.fa"),
+                        os.path.join(d, "in.bam"), "chrX:1-100"], env=env, capture_output=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 1 and r.stdout == b""
+    assert r.stderr.decode().count("Bad genome coordinates: chrX:1-100") == 1
+
+
 def _main(argv, capsys):
     rc = cli.main(argv)
     out = capsys.readouterr()

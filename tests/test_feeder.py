@@ -166,3 +166,59 @@ def test_pack_rejects_wide_k_in_u8():
         feed.pack(raw, raw["depth"].shape[1], feed.make_filter(13, 13, 0, 255))
     wide = feed.pack(raw, raw["depth"].shape[1], feed.make_filter(13, 13, 0, 900))
     assert wide["k"].dtype == np.uint16 and wide["k"].max() > 255
+
+
+def _crowded_bam(tmp_path):
+    """A pile deep enough for the pileup buffer's maxcnt (8000 reads, bam_pileup.c:375): 4000
+    reads on [60, 110) then 4100 on [100, 160), two samples, so which reads at 100 are kept
+    depends on whether the walk started before 110 (it then still holds the first pile)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from bamwriter import Read, write_bam
+    L = 400
+    reads = []
+    for i in range(8100):
+        pos, ln = (60, 50) if i < 4000 else (100, 60)
+        reads.append(Read(f"r{i}", 0, pos, 40, 16 * (i & 1), [("M", ln)], "ACGT" * (ln // 4) + "A" * (ln % 4),
+                          [30 + i % 7] * ln, {"RG": f"rg{i & 1}"}))
+    hdr = "@HD\tVN:1.0\tSO:coordinate\n@SQ\tSN:chr1\tLN:%d\n" % L
+    hdr += "".join(f"@RG\tID:rg{s}\tSM:s{s}\tPO:p{s}\n" for s in range(2))
+    path = str(tmp_path / "crowd.bam")
+    write_bam(path, hdr, [("chr1", L)], reads)
+    return path, ("ACGT" * (L // 4)).encode(), {"rg0": 0, "rg1": 1}
+
+
+def test_crowded_pileup_follows_the_reference_walks(tmp_path):
+    """Where the maxcnt drop depends on where a walk starts, pbf_pileup_mt gives what the
+    reference's own walks give: one fresh fetch + walk per window (pop_nucdiv.cpp:57-125), or
+    one walk of the region without windows -- for every piece size."""
+    path, seq, rg2s = _crowded_bam(tmp_path)
+    bam = feed.Bam(path)
+    beg, end, X = 0, 320, 20000
+
+    def reference_walks(win):
+        if win == 0:
+            return bam.pileup(0, beg, end, seq, rg2s, 2, X, -1)
+        depth, reads = [], []
+        a = beg
+        while a < end:
+            k = (a - beg) // win
+            wb, we = beg + k * win, beg + k * win + win - 1
+            sa, sb = (wb, min(we, end)) if a < we else (a, a + 1)
+            part = bam.pileup(0, sa, sb, seq, rg2s, 2, X, -1)
+            depth.append(part["depth"][a - sa:])
+            skip = int(part["depth"][:a - sa].sum())
+            reads.append(part["reads"][skip:])
+            a = sb
+        return {"depth": np.concatenate(depth), "reads": np.concatenate(reads)}
+
+    seen = set()
+    for win in (0, 64, 100, 37):
+        want = reference_walks(win)
+        seen.add(int(want["depth"][130].sum()))
+        for threads, chunk in [(1, 64), (3, 64), (2, 128), (4, 1 << 20)]:
+            got = bam.pileup(0, beg, end, seq, rg2s, 2, X, -1, threads=max(2, threads), chunk=chunk, win=win)
+            assert np.array_equal(got["depth"], want["depth"]), (win, threads, chunk)
+            assert np.array_equal(got["reads"], want["reads"]), (win, threads, chunk)
+    assert len(seen) > 1   # the fixture does reach maxcnt differently per walk start
+    bam.close()

@@ -16,7 +16,8 @@ from popbam_amd import shard
 CASES = [("g01_base", ["nucdiv", "-w", "1"], "chr1"), ("g12_regions", ["sfs", "-w", "2"], "chr1:777-14777"),
          ("g11_eleven", ["ld", "-w", "10"], "chr1"), ("g03_threepops", ["diverge", "-w", "1"], "chr1"),
          ("g12_regions", ["snp"], "chr1:2001-3000"), ("g02_interleaved", ["haplo", "-w", "1", "-o", "2"], "chr1"),
-         ("g01_base", ["tree", "-w", "1", "-d", "jc"], "chr1")]
+         ("g01_base", ["tree", "-w", "1", "-d", "jc"], "chr1"),
+         ("g13_snpformats", ["snp", "-o", "2", "-w", "2"], "chr1"), ("g14_onepop", ["snp", "-o", "2", "-w", "1"], "chr1")]
 
 
 def _windows(beg, end, w, windowed):
@@ -66,11 +67,24 @@ def test_slice_batch_rebases_reads():
         assert np.array_equal(ksub[f], kref[f]), f
 
 
-def _oracle_block(st, b, e):
+def _ms_header(text, ms):
+    """The oracle prints a block's own `snp -o 2` header; apply pbg_cmd.ms_windows to it
+    (> 0: the run's total window count, < 0: no header)."""
+    if not text.startswith("ms ") or ms == 0:
+        return text
+    head, rest = text.split("\n", 1)
+    if ms < 0:
+        return rest.split("\n", 2)[2]
+    f = head.split(" ")
+    f[2] = str(ms)
+    return " ".join(f) + "\n" + rest
+
+
+def _oracle_block(st, b, e, ms=0):
     c0 = (st.beg, st.end)
     st.beg, st.end = b, e
     try:
-        return harness.oracle_run(st)
+        return _ms_header(harness.oracle_run(st), ms)
     finally:
         st.beg, st.end = c0
 
@@ -82,8 +96,8 @@ def _worker(rank, world, port, results):
         for i, (name, args, region) in enumerate(CASES):
             st = harness.Setup(name, args, region)
             windowed = bool(st.opts.flag & harness.opt.BAM_WINDOW)
-            text = shard.run_sharded(lambda b, e: _oracle_block(st, b, e), st.beg, st.end, st.opts.win_size,
-                                     windowed)
+            text = shard.run_sharded(lambda b, e, ms: _oracle_block(st, b, e, ms), st.beg, st.end,
+                                     st.opts.win_size, windowed)
             if rank == 0:
                 results[i] = text
     finally:
@@ -127,8 +141,9 @@ def test_gpu_blocks_on_rebased_pileups(gpu_lib, world):
                 continue
             lo, hi = shard.positions_needed(reg[0], reg[1], st.opts.win_size, windowed)
             sub = shard.slice_batch(st.kbatch, 0, lo, max(hi, lo + 1))
+            ms = shard.ms_windows_for(st.beg, st.end, st.opts.win_size, windowed, r)
             parts.append(engine.run_command(st.opts, st.sm, st.chr, reg[0], reg[1], sub, pos0=sub["pos0"],
-                                            refid=st.refid))
+                                            refid=st.refid, ms_windows=ms))
         ours = "".join(parts)
         oob = harness.snp_oob_cells(harness.oracle_run(st)) if args[0] == "snp" else None
         ok, diff = harness.same_output(args, harness.oracle_run(st), ours, oob)
