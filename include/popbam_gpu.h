@@ -39,7 +39,9 @@
 extern "C" {
 #endif
 
-#define PBG_MAX_SAMPLES 64     /* u64 masks, as the reference (popbam.1:507-510)        */
+#define PBG_MAX_SAMPLES 126    /* the reference stops at 64 (u64 masks, popbam.1:507-510,
+                                  popbam.cpp:168); 65..126 use the two-word masks below and
+                                  16-byte rows (126 sample bits + counted + segregating)  */
 #define PBG_MAX_POPS    64     /* pop_mask[] is indexed by population (popbam.1:507-510) */
 #define PBG_SITE_BLOCK  64     /* positions per pbg_pileup.block_off entry                 */
 
@@ -71,6 +73,7 @@ typedef struct {
     int32_t  min_mapQ, min_baseQ;       /* -a -b (unsigned char in the reference); applied
                                            by the host when it builds the keys            */
     uint32_t flag;                      /* PBG_F_* bits                                   */
+    uint64_t pop_mask_hi[PBG_MAX_POPS]; /* samples 64..125 of each pop_mask (0 for n <= 64) */
 } pbg_params;
 
 /* Dense pileup batch for contiguous positions [pos0, pos0 + n_sites) of one contig, in the
@@ -99,7 +102,7 @@ typedef struct {
 } pbg_pileup;
 
 /* Row format written by pbg_call_sites: one little-endian word of W = 8*pbg_row_bytes()
- * bits per position (2 B for n<=14, 4 B for n<=30, 8 B for n<=62, 16 B for n<=64):
+ * bits per position (2 B for n<=14, 4 B for n<=30, 8 B for n<=62, 16 B for n<=126):
  *   bits 0..n-1  cal_site_type: sample derived & passing ((cb&3)==3)
  *   bit  W-2     counted: all n samples pass qfilter (popcount(sample_cov)==n)
  *   bit  W-1     segregating: counted and segbase() > 0

@@ -53,6 +53,17 @@ inline char nt16_char(unsigned char c) {
 
 inline unsigned popcnt64(uint64_t x) { return (unsigned)__builtin_popcountll(x); }
 
+// Sample masks: the reference's unsigned long long (popbam.cpp:168) holds n <= 64 samples.
+// The same algorithm runs here on 128-bit masks so that n <= 126 has a CPU statement too
+// (beyond 64 no reference output exists: parity there is unpinned).
+typedef unsigned __int128 mask_t;
+inline unsigned popcnt(mask_t x) { return popcnt64((uint64_t)x) + popcnt64((uint64_t)(x >> 64)); }
+inline mask_t pmask(const orc_params *p, int i) { return ((mask_t)p->pop_mask_hi[i] << 64) | p->pop_mask[i]; }
+inline int type_words(const orc_params *p) { return p->n_samples > 64 ? 2 : 1; }   // u64 per types[] entry
+inline mask_t load_type(const uint64_t *t, size_t pos, int tw) {
+    return tw == 2 ? ((mask_t)t[2 * pos + 1] << 64) | t[2 * pos] : (mask_t)t[pos];
+}
+
 // ---------------------------------------------------------------- LogGamma
 // gamma.cpp:126-166 (and Gamma, gamma.cpp:11-124).  cal_coef only calls it at integer
 // x in [1, 256]; for x < 12 Gamma() reduces an integer argument to y == 1 (so the rational
@@ -281,14 +292,14 @@ int segbase(int n, uint64_t *cb, char ref, int min_snpq) {
 }
 
 // ---------------------------------------------------------------- qfilter  pop_utils.cpp:102-120
-uint64_t qfilter(int n, uint64_t *cb, int min_rmsQ, int min_depth, int max_depth) {
-    uint64_t cov = 0;
+mask_t qfilter(int n, uint64_t *cb, int min_rmsQ, int min_depth, int max_depth) {
+    mask_t cov = 0;
     for (int i = 0; i < n; ++i) {
         unsigned short rms = (cb[i] >> 48) & 0xffff;
         unsigned short nr = (cb[i] >> 16) & 0xffff;
         if (rms >= min_rmsQ && nr >= min_depth && nr <= max_depth) {
             cb[i] |= 0x1ULL;
-            cov |= 0x1ULL << i;
+            cov |= (mask_t)1 << i;
         }
     }
     return cov;
@@ -297,7 +308,7 @@ uint64_t qfilter(int n, uint64_t *cb, int min_rmsQ, int min_depth, int max_depth
 // ---------------------------------------------------------------- per-window state (hData_t)
 struct Window {
     int beg = 0, end = 0, num_sites = 0, segsites = 0;
-    std::vector<uint64_t> types;               // popbamData::types, per counted site
+    std::vector<mask_t> types;                 // popbamData::types, per counted site
     std::vector<std::vector<uint64_t>> seq;    // hap.seq[sample][word]
     std::vector<unsigned> idx, pos;            // hap.idx / hap.pos per seg site
     std::vector<std::vector<uint16_t>> snpq, rms, nreads;
@@ -346,7 +357,7 @@ void do_nucdiv(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
         for (int j = i; j < np; j++) {
             for (int v = 0; v < n - 1; v++)
                 for (int w = v + 1; w < n; w++)
-                    if ((p->pop_mask[i] >> v & 1) && (p->pop_mask[j] >> w & 1)) {
+                    if ((pmask(p, i) >> v & 1) && (pmask(p, j) >> w & 1)) {
                         if (i == j) piw[i] += (double)d[v][w];
                         else pib[i * np + (j - (i + 1))] += (double)d[v][w];
                     }
@@ -397,11 +408,11 @@ void sfs_bins(const orc_params *p, const orc_cmd *c, const Window &W, int i, std
     sfs.assign(p->pop_n[i] + 1, 0);
     S = 0;
     for (int j = 0; j < W.segsites; j++) {
-        uint64_t t = W.types[W.idx[j]];
-        uint64_t pt = t & p->pop_mask[i];
+        mask_t t = W.types[W.idx[j]];
+        mask_t pt = t & pmask(p, i);
         unsigned short freq;
-        if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(p->pop_n[i] - popcnt64(pt));
-        else freq = (unsigned short)popcnt64(pt);
+        if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(p->pop_n[i] - popcnt(pt));
+        else freq = (unsigned short)popcnt(pt);
         ++sfs[freq];
         if (freq > 0 && freq < p->pop_n[i]) ++S;
     }
@@ -462,17 +473,17 @@ void do_ld(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
                 num_snps[j] = 0;
                 int count1 = 0, count2 = 0;
                 for (int i = 0; i < S - 1; i++) {
-                    uint64_t t1 = W.types[W.idx[i]] & p->pop_mask[j];
-                    unsigned m1 = popcnt64(t1);
+                    mask_t t1 = W.types[W.idx[i]] & pmask(p, j);
+                    unsigned m1 = popcnt(t1);
                     if (var(m1, j)) {
                         ++num_snps[j];
                         count2 = count1;
                         for (int k = i + 1; k < S; k++) {
-                            uint64_t t2 = W.types[W.idx[k]] & p->pop_mask[j];
-                            unsigned m2 = popcnt64(t2);
+                            mask_t t2 = W.types[W.idx[k]] & pmask(p, j);
+                            unsigned m2 = popcnt(t2);
                             if (var(m2, j)) {
                                 ++count2;
-                                r2[count1][count2] = r2_of(m1, m2, popcnt64(t1 & t2), p->pop_n[j]);
+                                r2[count1][count2] = r2_of(m1, m2, popcnt(t1 & t2), p->pop_n[j]);
                                 r2[count2][count1] = r2[count1][count2];
                             }
                         }
@@ -498,15 +509,15 @@ void do_ld(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
             }
     } else if (c->output == 2) {  // Wall's B and Q
         if (S >= 1) {
-            uint64_t last_type = 0;  // shared across populations (Appendix A.9)
+            mask_t last_type = 0;  // shared across populations (Appendix A.9)
             std::vector<int> cong(np, 0), part(np, 0);
-            std::vector<std::vector<uint64_t>> uniq(np);
+            std::vector<std::vector<mask_t>> uniq(np);
             for (int i = 0; i < S; i++)
                 for (int j = 0; j < np; j++) {
-                    uint64_t t = W.types[W.idx[i]];
-                    uint64_t type = t & p->pop_mask[j];
-                    uint64_t comp = ~t & p->pop_mask[j];
-                    if (type > 0 && type < p->pop_mask[j]) {
+                    mask_t t = W.types[W.idx[i]];
+                    mask_t type = t & pmask(p, j);
+                    mask_t comp = ~t & pmask(p, j);
+                    if (type > 0 && type < pmask(p, j)) {
                         if (num_snps[j] == 0) {
                             uniq[j].push_back(type);
                             last_type = type;
@@ -536,14 +547,14 @@ void do_ld(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
             for (int i = 0; i < np; i++) {
                 num_snps[i] = 0;
                 for (int j = 0; j < S - 1; j++) {
-                    uint64_t t1 = W.types[W.idx[j]] & p->pop_mask[i];
-                    unsigned m1 = popcnt64(t1);
+                    mask_t t1 = W.types[W.idx[j]] & pmask(p, i);
+                    unsigned m1 = popcnt(t1);
                     if (var(m1, i)) {
                         ++num_snps[i];
                         for (int k = j + 1; k < S; k++) {
-                            uint64_t t2 = W.types[W.idx[k]] & p->pop_mask[i];
-                            unsigned m2 = popcnt64(t2);
-                            if (var(m2, i)) val[i] += r2_of(m1, m2, popcnt64(t1 & t2), p->pop_n[i]);
+                            mask_t t2 = W.types[W.idx[k]] & pmask(p, i);
+                            unsigned m2 = popcnt(t2);
+                            if (var(m2, i)) val[i] += r2_of(m1, m2, popcnt(t1 & t2), p->pop_n[i]);
                         }
                     }
                 }
@@ -584,11 +595,11 @@ void do_diverge(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) 
             int segs = 0;
             uint16_t fixed = 0;
             for (int j = 0; j < W.segsites; j++) {
-                uint64_t t = W.types[W.idx[j]];
-                uint64_t pt = t & p->pop_mask[i];
+                mask_t t = W.types[W.idx[j]];
+                mask_t pt = t & pmask(p, i);
                 unsigned short freq;
-                if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(p->pop_n[i] - popcnt64(pt));
-                else freq = (unsigned short)popcnt64(pt);
+                if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(p->pop_n[i] - popcnt(pt));
+                else freq = (unsigned short)popcnt(pt);
                 if (freq > 0 && freq < p->pop_n[i]) ++segs;
                 else if (freq == p->pop_n[i]) ++fixed;
             }
@@ -624,7 +635,7 @@ void do_haplo(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
             if (nelem > 1) {
                 std::vector<int> b;
                 for (int j = 0; j < n; j++)
-                    if (p->pop_mask[i] >> j & 1) b.push_back(j);
+                    if (pmask(p, i) >> j & 1) b.push_back(j);
                 // local indices j,k index the GLOBAL diff matrix (Appendix A.11)
                 for (int j = 0; j < nelem - 1; j++)
                     for (int k = j + 1; k < nelem; k++)
@@ -648,21 +659,21 @@ void do_haplo(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
         nhaps_fn();
         for (int i = 0; i < np; i++) {
             if (p->pop_n[i] < 4) { ehhs[i] = std::numeric_limits<double>::quiet_NaN(); continue; }
-            std::list<uint64_t> pop_site;
+            std::list<mask_t> pop_site;
             for (int j = 0; j < W.segsites; j++) {
-                uint64_t pt = W.types[W.idx[j]] & p->pop_mask[i];
-                unsigned short popf = (unsigned short)popcnt64(pt);
+                mask_t pt = W.types[W.idx[j]] & pmask(p, i);
+                unsigned short popf = (unsigned short)popcnt(pt);
                 if (popf > 1 && popf < p->pop_n[i] - 1) pop_site.push_back(pt);
             }
             int part_max_count = 0;
-            uint64_t comp = 0, max_site = 0;
-            std::list<uint64_t> uniq(pop_site);
+            mask_t comp = 0, max_site = 0;
+            std::list<mask_t> uniq(pop_site);
             uniq.sort();
             uniq.unique();
-            for (uint64_t pt : uniq) {
+            for (mask_t pt : uniq) {
                 // ~CHECK_BIT(...) is always non-zero: comp accumulates pop_mask (A.11)
                 for (int j = 0; j < n; j++)
-                    if (p->pop_mask[i] >> j & 1) comp |= 0x1ULL << j;
+                    if (pmask(p, i) >> j & 1) comp |= (mask_t)1 << j;
                 int before = (int)pop_site.size();
                 pop_site.remove(pt);
                 pop_site.remove(comp);
@@ -670,7 +681,7 @@ void do_haplo(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
                 int part_count = (before - after) + 1;
                 if (part_count > part_max_count) { part_max_count = part_count; max_site = pt; }
             }
-            unsigned short popf = (unsigned short)popcnt64(max_site);
+            unsigned short popf = (unsigned short)popcnt(max_site);
             int pn = p->pop_n[i];
             double sh = (1.0 - ((double)((popf * popf) + ((pn - popf) * (pn - popf))) / (pn * pn))) * (double)(pn / (pn - 1));
             ehhs[i] = hdiv[i] / (1.0 - sh);
@@ -682,7 +693,7 @@ void do_haplo(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
                 if (i != j) minDxy[pi] = (uint16_t)0xFFFFFFFFu;  // UINT_MAX into u16 (A.7)
                 for (int v = 0; v < n - 1; v++)
                     for (int w = v + 1; w < n; w++)
-                        if ((p->pop_mask[i] >> v & 1) && (p->pop_mask[j] >> w & 1)) {
+                        if ((pmask(p, i) >> v & 1) && (pmask(p, j) >> w & 1)) {
                             if (i == j) piw[i] += (double)d[v][w];
                             else {
                                 pib[pi] += (double)d[v][w];
@@ -747,13 +758,13 @@ void do_snp(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
 void do_sweep(Out &o, const orc_params *p, const orc_cmd *c, const Window &W) {
     for (int i = 0; i < W.segsites; i++) {
         o.str(c->chr_name); o.str("\t"); o.i((long long)W.pos[i] + 1);
-        const uint64_t t = W.types[W.idx[i]];
+        const mask_t t = W.types[W.idx[i]];
         for (int j = 0; j < p->n_pops; j++) {
-            const uint64_t pt = t & p->pop_mask[j];
-            const unsigned short pop_n = (unsigned short)popcnt64(p->pop_mask[j]);
+            const mask_t pt = t & pmask(p, j);
+            const unsigned short pop_n = (unsigned short)popcnt(pmask(p, j));
             unsigned short freq;
-            if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(pop_n - popcnt64(pt));
-            else freq = (unsigned short)popcnt64(pt);
+            if ((p->flag & 0x40) && (t >> c->outidx & 1)) freq = (unsigned short)(pop_n - popcnt(pt));
+            else freq = (unsigned short)popcnt(pt);
             o.str("\t"); o.i(freq); o.str("\t"); o.i(pop_n);
         }
         o.str("\n");
@@ -792,14 +803,8 @@ void ms_header(Out &o, const orc_params *p, long nwindows) {
     o.str("\n1350154902\n\n");
 }
 
-struct SiteResult {
-    std::vector<uint64_t> cb, types;
-    std::vector<int16_t> fq;
-    std::vector<uint8_t> flags;
-};
-
 void call_range(const orc_params *p, uint32_t n_sites, const uint8_t *ref, const uint16_t *depth,
-                const uint32_t *reads, uint64_t *cb, uint64_t *types, int16_t *fq, uint8_t *flags) {
+                const uint32_t *reads, uint64_t *cb, mask_t *types, int16_t *fq, uint8_t *flags) {
     const int n = p->n_samples;
     std::vector<uint64_t> tmp(n);
     size_t off = 0;
@@ -809,7 +814,7 @@ void call_range(const orc_params *p, uint32_t n_sites, const uint8_t *ref, const
         size_t tot = 0;
         for (int j = 0; j < n; j++) tot += dp[j];
         uint8_t fl = 0;
-        uint64_t ty = 0;
+        mask_t ty = 0;
         int f = 0;
         if (!(ref[s] & 0x80)) {  // make_<cmd> only runs for positions the pileup called back
             fl |= 1;
@@ -817,11 +822,11 @@ void call_range(const orc_params *p, uint32_t n_sites, const uint8_t *ref, const
             char rch = (char)ref[s];
             if (!(p->flag & 0x20)) clean_heterozygotes(n, c, (int)rch, p->min_snpQ);
             f = segbase(n, c, rch, p->min_snpQ);
-            uint64_t cov = qfilter(n, c, p->min_rmsQ, p->min_depth, p->max_depth);
-            if ((int)popcnt64(cov) == n) {
+            mask_t cov = qfilter(n, c, p->min_rmsQ, p->min_depth, p->max_depth);
+            if ((int)popcnt(cov) == n) {
                 fl |= 2;
                 for (int i = 0; i < n; i++)
-                    if ((c[i] & 3ULL) == 3ULL) ty |= 1ULL << i;
+                    if ((c[i] & 3ULL) == 3ULL) ty |= (mask_t)1 << i;
                 if (f > 0) fl |= 4;
             }
         } else if (cb) {
@@ -834,7 +839,7 @@ void call_range(const orc_params *p, uint32_t n_sites, const uint8_t *ref, const
     }
 }
 
-void add_site(Window &W, const orc_params *p, uint32_t pos, uint64_t ty, uint8_t fl, const uint64_t *cb, char refc) {
+void add_site(Window &W, const orc_params *p, uint32_t pos, mask_t ty, uint8_t fl, const uint64_t *cb, char refc) {
     if (!(fl & 2)) return;
     int n = p->n_samples;
     W.types.push_back(ty);
@@ -1054,15 +1059,22 @@ const double *orc_lhet(void) { return tables().lhet.data(); }
 
 int orc_call_sites(const orc_params *p, uint32_t n_sites, const uint8_t *ref, const uint16_t *depth,
                    const uint32_t *reads, uint64_t *cb, uint64_t *types, int16_t *fq, uint8_t *flags) {
-    if (!p || p->n_samples < 1 || p->n_samples > 64) return -1;
-    call_range(p, n_sites, ref, depth, reads, cb, types, fq, flags);
+    if (!p || p->n_samples < 1 || p->n_samples > ORC_MAX_SAMPLES) return -1;
+    std::vector<mask_t> ty(types ? n_sites : 0);
+    call_range(p, n_sites, ref, depth, reads, cb, types ? ty.data() : nullptr, fq, flags);
+    const int tw = type_words(p);
+    if (types)
+        for (uint32_t s = 0; s < n_sites; s++) {
+            types[(size_t)s * tw] = (uint64_t)ty[s];
+            if (tw == 2) types[2 * (size_t)s + 1] = (uint64_t)(ty[s] >> 64);
+        }
     return 0;
 }
 
 // main_<cmd> window loop, e.g. pop_nucdiv.cpp:47-124
 long orc_run(const orc_params *p, const orc_cmd *c, uint32_t n_sites, const uint8_t *ref,
              const uint16_t *depth, const uint32_t *reads, char *out, size_t cap) {
-    if (!p || !c || p->n_samples < 1 || p->n_samples > 64) return -1;
+    if (!p || !c || p->n_samples < 1 || p->n_samples > ORC_MAX_SAMPLES) return -1;
     const int n = p->n_samples;
     int beg = c->beg, end = c->end;
     if (end > (int)n_sites) end = (int)n_sites;
@@ -1071,7 +1083,8 @@ long orc_run(const orc_params *p, const orc_cmd *c, uint32_t n_sites, const uint
     for (int s = 0; s < beg; s++)
         for (int j = 0; j < n; j++) off += depth[(size_t)s * n + j];
     int len = end > beg ? end - beg : 0;
-    std::vector<uint64_t> cb((size_t)len * n), types(len);
+    std::vector<uint64_t> cb((size_t)len * n);
+    std::vector<mask_t> types(len);
     std::vector<int16_t> fq(len);
     std::vector<uint8_t> flags(len);
     if (len) call_range(p, (uint32_t)len, ref + beg, depth + (size_t)beg * n, reads + off, cb.data(), types.data(), fq.data(), flags.data());
@@ -1107,9 +1120,11 @@ long orc_windows_from_sites(const orc_params *p, const orc_cmd *c, const uint64_
     SfsConst K = sfs_const(p->n_samples);
     Out o;
     Window W;
+    const int tw = type_words(p);
     for (uint32_t i = 0; i < n_win; i++) {
         init_window(W, p, wbeg[i], wend[i]);
-        for (int pos = wbeg[i]; pos < wend[i]; pos++) add_site(W, p, (uint32_t)pos, types[pos], flags[pos], nullptr, 0);
+        for (int pos = wbeg[i]; pos < wend[i]; pos++)
+            add_site(W, p, (uint32_t)pos, load_type(types, pos, tw), flags[pos], nullptr, 0);
         emit(o, p, c, W, K);
     }
     return finish(o, out, cap);
@@ -1124,9 +1139,11 @@ long orc_sfs_windows(const orc_params *p, const orc_cmd *c, const uint64_t *type
     SfsConst K = sfs_const(p->n_samples);
     Window W;
     const int np = p->n_pops;
+    const int tw = type_words(p);
     for (uint32_t w = 0; w < n_win; w++) {
         init_window(W, p, wbeg[w], wend[w]);
-        for (int pos = wbeg[w]; pos < wend[w]; pos++) add_site(W, p, (uint32_t)pos, types[pos], flags[pos], nullptr, 0);
+        for (int pos = wbeg[w]; pos < wend[w]; pos++)
+            add_site(W, p, (uint32_t)pos, load_type(types, pos, tw), flags[pos], nullptr, 0);
         for (int i = 0; i < np; i++) {
             std::vector<int> sfs;
             int S = 0;

@@ -13,7 +13,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("POPBAM_GPU_LIB") or os.path.join(HERE, "libpopbam_gpu.so")
 
-PBG_MAX_SAMPLES = 64
+PBG_MAX_SAMPLES = 126   # 64 in the reference (u64 masks); 65..126 on two-word masks
 PBG_MAX_POPS = 64
 PBG_SITE_BLOCK = 64
 
@@ -34,7 +34,15 @@ class PbgParams(C.Structure):
     _fields_ = [("n_samples", C.c_int32), ("n_pops", C.c_int32), ("pop_mask", C.c_uint64 * PBG_MAX_POPS),
                 ("pop_n", C.c_int32 * PBG_MAX_POPS), ("min_depth", C.c_int32), ("max_depth", C.c_int32),
                 ("min_rmsQ", C.c_int32), ("min_snpQ", C.c_int32), ("min_mapQ", C.c_int32),
-                ("min_baseQ", C.c_int32), ("flag", C.c_uint32)]
+                ("min_baseQ", C.c_int32), ("flag", C.c_uint32), ("pop_mask_hi", C.c_uint64 * PBG_MAX_POPS)]
+
+    def set_pop_mask(self, i: int, mask: int):
+        """Population i's sample mask (an int of up to PBG_MAX_SAMPLES bits) -> pop_mask /
+        pop_mask_hi."""
+        self.pop_mask[i], self.pop_mask_hi[i] = mask & ((1 << 64) - 1), mask >> 64
+
+    def get_pop_mask(self, i: int) -> int:
+        return int(self.pop_mask[i]) | (int(self.pop_mask_hi[i]) << 64)
 
 
 class PbgPileup(C.Structure):

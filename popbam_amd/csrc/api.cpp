@@ -110,7 +110,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     if (!out || !p) return fail(nullptr, PBG_E_ARG, "null argument");
     *out = nullptr;
     if (p->n_samples < 1 || p->n_samples > PBG_MAX_SAMPLES)
-        return fail(nullptr, PBG_E_ARG, "n_samples must be in [1, 64] (u64 sample masks, popbam.1:507-510)");
+        return fail(nullptr, PBG_E_ARG, "n_samples must be in [1, 126]");
     if (p->n_pops < 1 || p->n_pops > PBG_MAX_POPS) return fail(nullptr, PBG_E_ARG, "n_pops must be in [1, 64]");
     if (p->max_depth < 1 || p->max_depth > 65535) return fail(nullptr, PBG_E_ARG, "max_depth must be in [1, 65535]");
     int ndev = 0;
@@ -126,6 +126,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     d.npops = p->n_pops;
     for (int i = 0; i < PBG_MAX_POPS; ++i) {
         d.pop_mask[i] = i < p->n_pops ? p->pop_mask[i] : 0;
+        d.pop_mask_hi[i] = i < p->n_pops && p->n_samples > 64 ? p->pop_mask_hi[i] : 0;
         d.pop_n[i] = i < p->n_pops ? p->pop_n[i] : 0;
     }
     d.min_depth = p->min_depth;
@@ -140,7 +141,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     for (int v = 0; v < PBG_MAX_SAMPLES; ++v) d.sample_pop[v] = -1;
     for (int i = 0; i < p->n_pops; ++i)
         for (int v = 0; v < p->n_samples; ++v)
-            if ((p->pop_mask[i] >> v) & 1) {
+            if (((v < 64 ? p->pop_mask[i] >> v : d.pop_mask_hi[i] >> (v - 64)) & 1)) {
                 if (d.sample_pop[v] >= 0) {
                     delete c;
                     return fail(nullptr, PBG_E_ARG, "population masks overlap");
@@ -373,6 +374,7 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     // steady-state calls do not synchronise.
     const bool ld_ws = (o->stats & (PBG_S_OMEGA | PBG_S_WALL)) != 0;
     const int n = c->dp.n, np = c->dp.npops;
+    const uint64_t mw = c->row_bytes == 16 ? 2 : 1;
     bool known = false;
     for (const auto &pl : c->plans)
         known |= pl.wins == (const void *)wins && pl.n_win == n_win && pl.n_rows == n_rows && pl.stats == o->stats;
@@ -386,8 +388,9 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
             if (hw[i].beg < 0 || hw[i].end < hw[i].beg || (uint32_t)hw[i].end > n_rows)
                 return fail(c, PBG_E_RANGE, "window outside the row range");
             const uint64_t len = (uint64_t)(hw[i].end - hw[i].beg);
-            if (ld_ws || len > (uint64_t)pbg::kSegCap) worst += len + (uint64_t)n * (len / 64 + 1) + (ld_ws ? np * len : 0);
-            if (o->stats & PBG_S_ZNS) worst += np * len;
+            // words: masks are mw words each (two for 16-byte rows)
+            if (ld_ws || len > (uint64_t)pbg::kSegCap) worst += mw * len + (uint64_t)n * (len / 64 + 1) + (ld_ws ? mw * np * len : 0);
+            if (o->stats & PBG_S_ZNS) worst += mw * np * len;
         }
         constexpr uint64_t kPoolMax = 512ull << 20;   // words (4 GiB)
         const uint64_t want = std::max<uint64_t>(1024, std::min(worst, kPoolMax));
@@ -424,7 +427,7 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     A.seg_count = c->d_segcnt;
     A.var_count = c->d_segcnt + n_win;
     A.ld_ns = c->d_segcnt + n_win + (size_t)n_win * np;
-    A.lds = pbg::stats_lds_layout(n, np, c->dp.sfs_stride, o->stats, 0);
+    A.lds = pbg::stats_lds_layout(n, np, c->dp.sfs_stride, o->stats, 0, (int)mw);
     if (A.lds.bytes > 64 * 1024) return fail(c, PBG_E_ARG, "statistics need more LDS than a workgroup has");
     HIPCHK(c, pbg::launch_window_stats(c->row_bytes, c->dp, c->dt, rows, n_rows, n_win, A, (hipStream_t)stream));
     return PBG_OK;
@@ -554,13 +557,16 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
             HIPCHK(c, hipMemcpy(rows.data(), d_rows.p, rows.size(), hipMemcpyDeviceToHost));
             if (snp_words) HIPCHK(c, hipMemcpy(cb.data(), d_cb.p, cb.size() * 8, hipMemcpyDeviceToHost));
         }
-        const uint64_t tmask = n >= 64 ? ~0ULL : (1ULL << n) - 1;
+        using pbg::mask128;
+        const mask128 tmask = ((mask128)1 << n) - 1;   // n <= 126
+        std::vector<mask128> pmask(np);
+        for (int i = 0; i < np; ++i) pmask[i] = ((mask128)c->dp.pop_mask_hi[i] << 64) | c->dp.pop_mask[i];
         // print_ms prints its header in the window loop at cw == 0 (pop_snp.cpp:114-115): not at
         // all without windows; a block of a longer run passes the run's count or suppresses it
         if (cmd->output == 2 && cmd->ms_windows >= 0 && !win.empty())
             pbg::format_ms_header(text, n, np, c->params.pop_n, cmd->ms_windows > 0 ? (long)cmd->ms_windows : (long)win.size());
         std::vector<int32_t> wpos;
-        std::vector<uint64_t> wtypes;
+        std::vector<mask128> wtypes;
         for (auto &x : win) {
             wpos.clear();
             wtypes.clear();
@@ -568,13 +574,13 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
                 const size_t i = (size_t)(p - dpos0);
                 const unsigned char *r = rows.data() + i * rb;
                 if (!((r[rb - 1] >> 7) & 1)) continue;   // not segregating
-                uint64_t types = 0;
-                for (int b = 0; b < std::min(rb, 8); ++b) types |= (uint64_t)r[b] << (8 * b);
+                mask128 types = 0;
+                for (int b = 0; b < rb; ++b) types |= (mask128)r[b] << (8 * b);
                 types &= tmask;
                 if (cmd->output == 0)
                     pbg::format_snp_site(text, *cmd, n, (int32_t)p, hp->ref[p - pos0] & 0x7f, cb.data() + i * n);
                 else if (cmd->output == 1)
-                    pbg::format_sweep_site(text, *cmd, np, c->params.pop_mask, c->params.flag, (int32_t)p, types);
+                    pbg::format_sweep_site(text, *cmd, np, pmask.data(), c->params.flag, (int32_t)p, types);
                 wpos.push_back((int32_t)p);
                 wtypes.push_back(types);
             }

@@ -390,18 +390,17 @@ void format_snp_site(std::string &out, const pbg_cmd &c, int n, int32_t pos, uns
 
 // snp -o 1: print_sweep (pop_snp.cpp:243-268).  At a counted site every sample passes
 // qfilter, so the reference's pop_sample_mask (sample_cov & pop_mask) is pop_mask.
-void format_sweep_site(std::string &out, const pbg_cmd &c, int np, const uint64_t *pop_mask, uint32_t flag,
-                       int32_t pos, uint64_t types) {
+void format_sweep_site(std::string &out, const pbg_cmd &c, int np, const mask128 *pop_mask, uint32_t flag,
+                       int32_t pos, mask128 types) {
     W o{out};
     o.t(c.chr_name);
     o.t("\t");
     o.i((long long)pos + 1);
     for (int j = 0; j < np; j++) {
-        const uint64_t pt = types & pop_mask[j];
-        const unsigned pop_n = (unsigned)__builtin_popcountll(pop_mask[j]);
+        const mask128 pt = types & pop_mask[j];
+        const unsigned pop_n = (unsigned)popcount128(pop_mask[j]);
         const bool flip = (flag & PBG_F_OUTGROUP) && ((types >> c.outidx) & 1);
-        const unsigned freq = (unsigned short)(flip ? pop_n - (unsigned)__builtin_popcountll(pt)
-                                                    : (unsigned)__builtin_popcountll(pt));
+        const unsigned freq = (unsigned short)(flip ? pop_n - (unsigned)popcount128(pt) : (unsigned)popcount128(pt));
         o.t("\t");
         o.i(freq);
         o.t("\t");
@@ -435,7 +434,7 @@ void format_ms_header(std::string &out, int n, int np, const int32_t *pop_n, lon
 // the window as std::setprecision(8) (printf "%.8g"), then one 0/1 string per sample, the
 // derived bit flipped where the outgroup carries it.
 void format_ms_window(std::string &out, int n, uint32_t flag, int outidx, int32_t wbeg, int32_t wend,
-                      const std::vector<int32_t> &pos, const std::vector<uint64_t> &types) {
+                      const std::vector<int32_t> &pos, const std::vector<mask128> &types) {
     W o{out};
     const size_t S = pos.size();
     o.t("//\nsegsites: ");

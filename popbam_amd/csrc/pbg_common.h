@@ -16,6 +16,7 @@ constexpr int kSiteBlock = PBG_SITE_BLOCK;
 struct DevParams {
     int32_t n, npops;
     uint64_t pop_mask[PBG_MAX_POPS];
+    uint64_t pop_mask_hi[PBG_MAX_POPS];   // samples 64..125 (n > 64)
     int32_t pop_n[PBG_MAX_POPS];
     int32_t min_depth, max_depth, min_rmsQ, min_snpQ, min_mapQ, min_baseQ;
     uint32_t flag;
@@ -116,7 +117,7 @@ struct WinLds {
     int32_t planecap;   // bitplane words in LDS (n * kSegCap / 64)
     int32_t r2lds;      // doubles of the r^2 tables copied to LDS (0: read from HBM / L2)
 };
-WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_total);
+WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_total, int mask_words);
 
 struct StatsArgs {
     uint32_t stats;

@@ -29,10 +29,13 @@ void format_window(std::string &out, const pbg_cmd &cmd, int n_samples, int n_po
 // print_popbam_snp (pop_snp.cpp:224-241) for one position's consensus words
 void format_snp_site(std::string &out, const pbg_cmd &cmd, int n_samples, int32_t pos, unsigned char refc,
                      const uint64_t *cb);
-void format_sweep_site(std::string &out, const pbg_cmd &cmd, int n_pops, const uint64_t *pop_mask, uint32_t flag,
-                       int32_t pos, uint64_t types);
+// sample masks of up to PBG_MAX_SAMPLES bits (the reference's u64 for n <= 64)
+typedef unsigned __int128 mask128;
+inline int popcount128(mask128 x) { return __builtin_popcountll((uint64_t)x) + __builtin_popcountll((uint64_t)(x >> 64)); }
+void format_sweep_site(std::string &out, const pbg_cmd &cmd, int n_pops, const mask128 *pop_mask, uint32_t flag,
+                       int32_t pos, mask128 types);
 void format_ms_header(std::string &out, int n_samples, int n_pops, const int32_t *pop_n, long n_windows);
 void format_ms_window(std::string &out, int n_samples, uint32_t flag, int outidx, int32_t wbeg, int32_t wend,
-                      const std::vector<int32_t> &pos, const std::vector<uint64_t> &types);
+                      const std::vector<int32_t> &pos, const std::vector<mask128> &types);
 
 }  // namespace pbg

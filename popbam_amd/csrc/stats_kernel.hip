@@ -28,6 +28,33 @@ namespace {
 
 __device__ __forceinline__ unsigned pc(uint64_t x) { return (unsigned)__popcll(x); }
 
+// The sample bits of a row: one u64 for 2 / 4 / 8-byte rows, two for 16-byte rows (n <= 126;
+// the reference's masks are one u64, n <= 64, popbam.cpp:168).  Every statistic below is
+// written once over the mask type M: a bitwise and / complement, equality, the unsigned order
+// (std::list::sort in calc_ehhs), popcount and a bit test.
+struct M2 {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ M2 operator&(M2 a, M2 b) { return {a.lo & b.lo, a.hi & b.hi}; }
+__device__ __forceinline__ M2 operator~(M2 a) { return {~a.lo, ~a.hi}; }
+__device__ __forceinline__ bool operator==(M2 a, M2 b) { return a.lo == b.lo && a.hi == b.hi; }
+__device__ __forceinline__ bool operator<(M2 a, M2 b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
+__device__ __forceinline__ unsigned pc(M2 x) { return pc(x.lo) + pc(x.hi); }
+__device__ __forceinline__ bool nonzero(uint64_t x) { return x != 0; }
+__device__ __forceinline__ bool nonzero(M2 x) { return (x.lo | x.hi) != 0; }
+__device__ __forceinline__ uint32_t bit(uint64_t x, int v) { return (uint32_t)(x >> v) & 1u; }
+__device__ __forceinline__ uint32_t bit(M2 x, int v) { return (uint32_t)(v < 64 ? x.lo >> v : x.hi >> (v - 64)) & 1u; }
+template <class M>
+__device__ __forceinline__ M pop_mask(const DevParams &P, int i);
+template <>
+__device__ __forceinline__ uint64_t pop_mask<uint64_t>(const DevParams &P, int i) { return P.pop_mask[i]; }
+template <>
+__device__ __forceinline__ M2 pop_mask<M2>(const DevParams &P, int i) { return {P.pop_mask[i], P.pop_mask_hi[i]}; }
+template <int RB>
+struct RowMask { using T = uint64_t; };
+template <>
+struct RowMask<16> { using T = M2; };
+
 // x86 SSE produces the "default NaN" (sign bit set) for invalid operations; glibc prints it
 // as "-nan".  Canonicalise device NaNs the same way before they reach the formatter.
 __device__ __forceinline__ double x86nan(double v) { return (v != v) ? __longlong_as_double(0xFFF8000000000000LL) : v; }
@@ -50,9 +77,11 @@ __device__ __forceinline__ int wave_sum(int v) {
 
 // Row r (0 .. 16/RB - 1) of a 16-byte word of RB-byte rows (include/popbam_gpu.h row format).
 template <int RB>
-__device__ __forceinline__ void row_in_word(const uint4 &q, int r, uint64_t &types, bool &counted, bool &seg) {
+__device__ __forceinline__ void row_in_word(const uint4 &q, int r, typename RowMask<RB>::T &types, bool &counted,
+                                            bool &seg) {
     if constexpr (RB == 16) {
-        types = (uint64_t)q.x | ((uint64_t)q.y << 32);
+        types.lo = (uint64_t)q.x | ((uint64_t)q.y << 32);
+        types.hi = ((uint64_t)q.z | ((uint64_t)q.w << 32)) & 0x3FFFFFFFFFFFFFFFULL;
         counted = (q.w >> 30) & 1u;
         seg = (q.w >> 31) & 1u;
     } else {
@@ -70,7 +99,7 @@ __device__ __forceinline__ void row_in_word(const uint4 &q, int r, uint64_t &typ
 
 }  // namespace
 
-WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_total) {
+WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_total, int mask_words) {
     WinLds L{};
     uint32_t b = 0;
     auto take = [&](uint32_t bytes) {
@@ -80,7 +109,7 @@ WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_to
     };
     const bool planes = stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE);
     const bool diff = stats & (PBG_S_NUCDIV | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE);
-    L.seg = take(kSegCap * 8);
+    L.seg = take(kSegCap * 8 * mask_words);
     L.var = take(0);
     L.planecap = planes ? n * (kSegCap / 64) : 0;
     L.plane = take((uint32_t)L.planecap * 8);
@@ -99,11 +128,13 @@ WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_to
 template <int RB>
 __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables T, const void *__restrict__ rows,
                                                           uint32_t n_rows, uint32_t n_win, StatsArgs A) {
+    using M = typename RowMask<RB>::T;
+    constexpr uint64_t NW = sizeof(M) / 8;   // pool words per mask
     extern __shared__ __align__(16) unsigned char sm[];
     const uint32_t w = blockIdx.x;
     if (w >= n_win) return;
     const WinLds &L = A.lds;
-    uint64_t *s_seg = reinterpret_cast<uint64_t *>(sm + L.seg);
+    M *s_seg = reinterpret_cast<M *>(sm + L.seg);
     uint64_t *s_plane = reinterpret_cast<uint64_t *>(sm + L.plane);
     uint16_t *s_diff = reinterpret_cast<uint16_t *>(sm + L.diff);
     int32_t *s_acc = reinterpret_cast<int32_t *>(sm + L.acc);
@@ -141,12 +172,12 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         return q;
     };
     // seg rows of word c (in window): bit mask + types; `store` gets (index, types)
-    auto compact = [&](uint64_t *dst, uint32_t cap, bool count_sites, int &my_counted) -> uint32_t {
+    auto compact = [&](M *dst, uint32_t cap, bool count_sites, int &my_counted) -> uint32_t {
         uint32_t S = 0;
         for (int64_t cb = c0; cb < c1; cb += 64) {
             const int64_t c = cb + lane;
             const uint4 q = load_word(c);
-            uint64_t t[R];
+            M t[R];
             uint32_t segm = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -177,12 +208,14 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     const bool need_planes = (stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY |
                                        PBG_S_TREE)) != 0;
     const bool need_diff = (stats & (PBG_S_NUCDIV | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE)) != 0;
-    // pool slice: [seg rows: S][bitplanes: n*nwords, when they outgrow LDS][omega / Wall lists: np*S]
+    // pool slice (u64 words): [seg rows: S masks][bitplanes: n*nwords, when they outgrow LDS]
+    // [omega / Wall lists: np*S masks]
     const bool over = S > (uint32_t)kSegCap;
-    uint64_t *wsg = nullptr, *wpl = nullptr;
+    M *wsg = nullptr;
+    uint64_t *wpl = nullptr;
     if (over || ld_ws) {
-        const uint64_t npl = (over && need_planes) ? (uint64_t)n * nwords : 0, nli = ld_ws ? (uint64_t)np * S : 0;
-        const uint64_t size = S + npl + nli;
+        const uint64_t npl = (over && need_planes) ? (uint64_t)n * nwords : 0, nli = ld_ws ? (uint64_t)np * S * NW : 0;
+        const uint64_t size = S * NW + npl + nli;
         unsigned long long off = 0;
         if (lane == 0) {
             off = atomicAdd(A.pool_used, (unsigned long long)size);
@@ -191,7 +224,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                 off = ~0ULL;
             } else {
                 A.win_off[2 * w] = off;
-                A.win_off[2 * w + 1] = off + S + npl;
+                A.win_off[2 * w + 1] = off + S * NW + npl;
             }
         }
         off = __shfl(off, 0, 64);
@@ -199,8 +232,8 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
             if (lane == 0 && A.seg_count) A.seg_count[w] = 0;
             return;
         }
-        wsg = A.pool + off;
-        wpl = wsg + S;
+        wsg = reinterpret_cast<M *>(A.pool + off);
+        wpl = A.pool + off + S * NW;
         __syncthreads();
         if (over) {
             int unused = 0;
@@ -210,7 +243,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         }
     }
     __syncthreads();
-    auto seg_at = [&](uint32_t j) -> uint64_t { return j < (uint32_t)kSegCap ? s_seg[j] : wsg[j]; };
+    auto seg_at = [&](uint32_t j) -> M { return j < (uint32_t)kSegCap ? s_seg[j] : wsg[j]; };
 
     const pbg_window_out &O = A.out;
     if (lane == 0) {
@@ -227,9 +260,9 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         // plane[v*nwords + k] bit b = sample v derived at segregating site 64k+b (hap.seq)
         for (int k = 0; k < nwords; ++k) {
             const uint32_t j = (uint32_t)(k * 64 + lane);
-            const uint64_t t = j < S ? seg_at(j) : 0;
+            const M t = j < S ? seg_at(j) : M{};
             for (int v = 0; v < n; ++v) {
-                const uint64_t m = __ballot((t >> v) & 1);
+                const uint64_t m = __ballot(bit(t, v));
                 if (lane == 0) plane[v * nwords + k] = m;
             }
         }
@@ -293,10 +326,10 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         for (int i = lane; i < np * bstride; i += 64) s_bins[i] = 0;
         __syncthreads();
         for (uint32_t j = (uint32_t)lane; j < S; j += 64) {
-            const uint64_t t = seg_at(j);
-            const bool flip = (P.flag & PBG_F_OUTGROUP) && ((t >> A.outidx) & 1);
+            const M t = seg_at(j);
+            const bool flip = (P.flag & PBG_F_OUTGROUP) && bit(t, A.outidx);
             for (int i = 0; i < np; ++i) {
-                const unsigned f = pc(t & P.pop_mask[i]);
+                const unsigned f = pc(t & pop_mask<M>(P, i));
                 const unsigned freq = flip ? (unsigned)(uint16_t)(P.pop_n[i] - (int)f) : f;
                 atomicAdd(&s_bins[i * bstride + (int)freq], 1);
             }
@@ -354,7 +387,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         // counts first (one pool allocation per window), then the lists
         uint32_t tot = 0;
         for (int i = 0; i < np; ++i) {
-            const uint64_t pm = P.pop_mask[i];
+            const M pm = pop_mask<M>(P, i);
             const int nn = P.pop_n[i], mf = A.min_freq;
             uint32_t V = 0;
             int lastvar = 0;
@@ -380,8 +413,8 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         }
         unsigned long long off = 0;
         if (lane == 0 && tot) {
-            off = atomicAdd(A.pool_used, (unsigned long long)tot);
-            if (off + tot > A.pool_cap) {
+            off = atomicAdd(A.pool_used, (unsigned long long)(tot * NW));
+            if (off + tot * NW > A.pool_cap) {
                 atomicOr(A.err, 4);
                 off = ~0ULL;
             }
@@ -389,7 +422,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         off = __shfl(off, 0, 64);
         __syncthreads();
         for (int i = 0; i < np; ++i) {
-            const uint64_t pm = P.pop_mask[i];
+            const M pm = pop_mask<M>(P, i);
             const int nn = P.pop_n[i], mf = A.min_freq;
             const uint32_t Vi = (uint32_t)s_vc[i];
             if (lane == 0) A.zoff[(size_t)w * np + i] = off;
@@ -397,11 +430,11 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                 if (lane == 0) A.var_count[(size_t)w * np + i] = 0;
                 continue;
             }
-            uint64_t *vl = A.pool + off;
+            M *vl = reinterpret_cast<M *>(A.pool + off);
             uint32_t V = 0;
             for (uint32_t c0 = 0; c0 < S; c0 += 64) {
                 const uint32_t j = c0 + (uint32_t)lane;
-                uint64_t t = 0;
+                M t{};
                 bool v = false;
                 if (j < S) {
                     t = seg_at(j) & pm;
@@ -412,7 +445,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                 if (v) vl[V + (uint32_t)__popcll(bm & ((1ULL << lane) - 1))] = t;
                 V += (uint32_t)__popcll(bm);
             }
-            off += Vi;
+            off += Vi * NW;
         }
     }
 
@@ -455,7 +488,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
             if (nelem > 1) {
                 int c = 0;
                 for (int j = 0; j < n; j++)
-                    if ((P.pop_mask[i] >> j) & 1) b[c++] = j;
+                    if (P.sample_pop[j] == i) b[c++] = j;
                 // local indices j,k index the global diff matrix (A.11)
                 for (int j = 0; j < nelem - 1; j++)
                     for (int k = j + 1; k < nelem; k++)
@@ -483,11 +516,11 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                 } else {
                     // max multiplicity among non-singleton partitions, ties -> smallest value
                     // (std::list sort + unique + remove, pop_haplo.cpp:273-313)
-                    const uint64_t pm = P.pop_mask[i];
+                    const M pm = pop_mask<M>(P, i);
                     int best = 0;
-                    uint64_t max_site = 0;
+                    M max_site{};
                     for (uint32_t j = 0; j < S; j++) {
-                        const uint64_t pt = seg_at(j) & pm;
+                        const M pt = seg_at(j) & pm;
                         const unsigned f = pc(pt);
                         if (!(f > 1 && (int)f < nelem - 1)) continue;
                         int cnt = 0;
@@ -513,7 +546,9 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
 // Serial LD chains, one lane per chain (pop_ld.cpp:254-458), reading the ordered segregating
 // lists window_stats_kernel copied into the pool.  Lanes of a wave belong to
 // different windows, so the dependent double additions of 64 chains overlap.
+template <class M>
 __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A) {
+    constexpr uint64_t NW = sizeof(M) / 8;
     __shared__ double s_r2[4096];
     const int np = P.npops;
     int r2_total = 0;
@@ -530,18 +565,19 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
         const uint32_t w = gid;
         if (w >= n_win) return;
         const int S = A.seg_count[w];
-        const uint64_t *seg = A.pool + A.win_off[2 * w];
+        const M *seg = reinterpret_cast<const M *>(A.pool + A.win_off[2 * w]);
         int ns[PBG_MAX_POPS], cong[PBG_MAX_POPS], part[PBG_MAX_POPS], nu[PBG_MAX_POPS];
         for (int j = 0; j < np; j++) ns[j] = cong[j] = part[j] = nu[j] = 0;
-        uint64_t *uniq = A.pool + A.win_off[2 * w + 1];   // np slices of S
-        uint64_t last_type = 0;
+        M *uniq = reinterpret_cast<M *>(A.pool + A.win_off[2 * w + 1]);   // np slices of S
+        M last_type{};
         for (int i = 0; i < S; i++) {
-            const uint64_t t = seg[i];
+            const M t = seg[i];
             for (int j = 0; j < np; j++) {
-                const uint64_t type = t & P.pop_mask[j];
-                const uint64_t comp = ~t & P.pop_mask[j];
-                uint64_t *u = uniq + (uint64_t)j * (uint64_t)S;
-                if (type > 0 && type < P.pop_mask[j]) {
+                const M pm = pop_mask<M>(P, j);
+                const M type = t & pm;
+                const M comp = ~t & pm;
+                M *u = uniq + (uint64_t)j * (uint64_t)S;
+                if (nonzero(type) && type < pm) {
                     if (ns[j] == 0) {
                         u[nu[j]++] = type;
                         last_type = type;
@@ -578,9 +614,9 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
     const uint32_t w = gid / np;
     const int i = (int)(gid - w * np);
     const int S = A.seg_count[w];
-    const uint64_t *seg = A.pool + A.win_off[2 * w];
+    const M *seg = reinterpret_cast<const M *>(A.pool + A.win_off[2 * w]);
     const int nn = P.pop_n[i], np1 = nn + 1, mf = A.min_freq;
-    const uint64_t pm = P.pop_mask[i];
+    const M pm = pop_mask<M>(P, i);
     const double *r2p = r2tab + T.r2_off[i];
     auto variable = [&](unsigned m) { return (int)m >= mf && (int)m <= nn - mf; };
     int ns = 0;
@@ -588,9 +624,9 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
     {   // calc_omegamax pop_ld.cpp:254-373 (sums accumulate across partitions, A.8)
         if (S >= 1) {
             int V = 0;
-            uint64_t *vt = A.pool + A.win_off[2 * w + 1] + (uint64_t)i * (uint64_t)S;
+            M *vt = reinterpret_cast<M *>(A.pool + A.win_off[2 * w + 1] + (uint64_t)i * (uint64_t)S * NW);
             for (int j = 0; j < S; j++) {
-                const uint64_t t = seg[j] & pm;
+                const M t = seg[j] & pm;
                 if (variable(pc(t))) {
                     if (j < S - 1) ++ns;
                     vt[V++] = t;
@@ -599,7 +635,7 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
             ++ns;
             auto r2 = [&](int a, int b) -> double {   // a < b; 0 beyond the variable sites
                 if (b >= V) return 0.0;
-                const uint64_t ta = vt[a], tb = vt[b];
+                const M ta = vt[a], tb = vt[b];
                 return r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
             };
             double sl = 0, sr = 0, sb = 0;
@@ -635,41 +671,47 @@ __device__ __forceinline__ double quad_bcast(double x) {
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), K * 0x55, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
-constexpr int kZnsStage = 256;   // list entries of a chain staged in LDS (longer lists: read from the pool)
+// list entries of a chain staged in LDS (longer lists: read from the pool), and the slot
+// stride: +16 B staggers the slots' LDS banks
+template <class M>
+constexpr int zns_stage() { return sizeof(M) == 8 ? 256 : 128; }
+template <class M>
+constexpr int zns_stride() { return zns_stage<M>() + (sizeof(M) == 8 ? 2 : 1); }
 constexpr int kZnsUnroll = 4;    // steps whose loads are issued before their adds (latency hiding)
-constexpr int kZnsStride = kZnsStage + 2;   // u64 per chain slot: +16 B staggers the slots' LDS banks
+template <class M>
 __global__ __launch_bounds__(64) void window_zns_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A,
                                                         int r2_lds) {
+    constexpr int kZnsStage = zns_stage<M>(), kZnsStride = zns_stride<M>();
     extern __shared__ __align__(16) double s_dyn[];
     double *s_r2t = s_dyn;                                                      // [r2_lds]
-    uint64_t *s_t = reinterpret_cast<uint64_t *>(s_dyn + r2_lds);              // [16][kZnsStride] types
+    M *s_t = reinterpret_cast<M *>(s_dyn + r2_lds);                            // [16][kZnsStride] masks
     for (int i = threadIdx.x; i < r2_lds; i += 64) s_r2t[i] = T.r2[i];
     const int np = P.npops;
     const int lane = threadIdx.x, g = lane & 3, q = lane >> 2;
     const uint32_t nch = n_win * (uint32_t)np;
     const uint32_t ch = blockIdx.x * 16 + (uint32_t)q;
     int V = 0;
-    const uint64_t *L = A.pool;
+    const M *L = reinterpret_cast<const M *>(A.pool);
     int np1 = 1, r2o = 0;
     if (ch < nch) {
         const uint32_t w = ch / (uint32_t)np;
         const int i = (int)(ch - w * (uint32_t)np);
         V = A.var_count[ch];
-        L = A.pool + A.zoff[ch];
+        L = reinterpret_cast<const M *>(A.pool + A.zoff[ch]);
         np1 = P.pop_n[i] + 1;
         r2o = T.r2_off[i];
     }
     // all chains of the wave staged in LDS, or all read from the pool (wave-uniform, so every
     // load below has a known address space: ds_read, not flat)
     const bool staged = !__ballot(V > kZnsStage);
-    uint64_t *lt = s_t + q * kZnsStride;
+    M *lt = s_t + q * kZnsStride;
     if (staged)
         for (int j = g; j < V; j += 4) lt[j] = L[j];
     __syncthreads();
     // row a, pairs b = b0 + g (b0 = a+1, a+5, ...); lanes past the row end add +0.0.  Branch-free:
     // every step's list loads depend only on the (a, b0) arithmetic, so the loads of all
     // kZnsUnroll steps issue before the first add waits on them.
-    auto run = [&](const uint64_t *lst, const double *r2p) -> double {
+    auto run = [&](const M *lst, const double *r2p) -> double {
         const int vm1 = V > 0 ? V - 1 : 0;
         int a = 0, b0 = 1;
         double acc = 0.0;
@@ -690,8 +732,8 @@ __global__ __launch_bounds__(64) void window_zns_kernel(DevParams P, DevTables T
             double r[kZnsUnroll];
 #pragma unroll
             for (int u = 0; u < kZnsUnroll; ++u) {
-                const uint64_t ta = lst[ia[u]], tb = lst[ib[u]];
-                const double rv = r2p[((int)__popcll(ta) * np1 + (int)__popcll(tb)) * np1 + (int)__popcll(ta & tb)];
+                const M ta = lst[ia[u]], tb = lst[ib[u]];
+                const double rv = r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
                 r[u] = ok[u] ? rv : 0.0;
             }
 #pragma unroll
@@ -741,15 +783,21 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
         for (int i = 0; i < P.npops; ++i) r2_total += (P.pop_n[i] + 1) * (P.pop_n[i] + 1) * (P.pop_n[i] + 1);
         const int r2_lds = r2_total <= 4608 ? r2_total : 0;   // <= 36 KB of LDS per wave
         const uint32_t chains = n_win * (uint32_t)P.npops;
-        const size_t lds = (size_t)r2_lds * sizeof(double) + 16 * kZnsStride * 8;
-        hipLaunchKernelGGL(window_zns_kernel, dim3((chains + 15) / 16), dim3(64), lds, stream, P, T, n_win, A, r2_lds);
+        const dim3 g((chains + 15) / 16);
+        if (rb == 16)
+            hipLaunchKernelGGL(window_zns_kernel<M2>, g, dim3(64), (size_t)r2_lds * 8 + 16 * zns_stride<M2>() * 16, stream,
+                               P, T, n_win, A, r2_lds);
+        else
+            hipLaunchKernelGGL(window_zns_kernel<uint64_t>, g, dim3(64), (size_t)r2_lds * 8 + 16 * zns_stride<uint64_t>() * 8,
+                               stream, P, T, n_win, A, r2_lds);
     }
     const uint32_t ld = A.stats & (PBG_S_OMEGA | PBG_S_WALL);
     if (ld) {
         if (ld != PBG_S_OMEGA && ld != PBG_S_WALL) return hipErrorInvalidValue;
         const uint32_t chains = (ld == PBG_S_WALL) ? n_win : n_win * (uint32_t)P.npops;
-        hipLaunchKernelGGL(window_ld_kernel, dim3((chains + kBlockThreads - 1) / kBlockThreads), dim3(kBlockThreads), 0,
-                           stream, P, T, n_win, A);
+        const dim3 g((chains + kBlockThreads - 1) / kBlockThreads);
+        if (rb == 16) hipLaunchKernelGGL(window_ld_kernel<M2>, g, dim3(kBlockThreads), 0, stream, P, T, n_win, A);
+        else hipLaunchKernelGGL(window_ld_kernel<uint64_t>, g, dim3(kBlockThreads), 0, stream, P, T, n_win, A);
     }
     return hipGetLastError();
 }

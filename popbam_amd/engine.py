@@ -20,11 +20,14 @@ from . import options as opt
 def make_params(o: opt.Options, sm: opt.SampleModel) -> _lib.PbgParams:
     masks, counts = sm.pop_masks()
     if len(masks) > _lib.PBG_MAX_POPS:
-        raise opt.PopbamError("more than 16 populations")
+        raise opt.PopbamError(f"more than {_lib.PBG_MAX_POPS} populations")
+    if sm.n > _lib.PBG_MAX_SAMPLES:
+        raise opt.PopbamError(f"more than {_lib.PBG_MAX_SAMPLES} samples")
     p = _lib.PbgParams()
     p.n_samples, p.n_pops = sm.n, len(masks)
     for i, (m, c) in enumerate(zip(masks, counts)):
-        p.pop_mask[i], p.pop_n[i] = m, c
+        p.set_pop_mask(i, m)
+        p.pop_n[i] = c
     p.min_depth, p.max_depth = o.min_depth, o.max_depth
     p.min_rmsQ, p.min_snpQ = o.min_rmsQ, o.min_snpQ
     p.min_mapQ, p.min_baseQ = o.min_mapQ & 0xFF, o.min_baseQ & 0xFF

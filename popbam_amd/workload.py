@@ -31,10 +31,13 @@ def default_params(n_samples: int, n_pops: int = 2, **kw) -> _lib.PbgParams:
     p = _lib.PbgParams()
     p.n_samples, p.n_pops = n_samples, n_pops
     per = n_samples // n_pops
+    masks = [0] * n_pops
     for i in range(n_samples):
         pi = min(i // per, n_pops - 1)
-        p.pop_mask[pi] |= 1 << i
+        masks[pi] |= 1 << i
         p.pop_n[pi] += 1
+    for pi, m in enumerate(masks):
+        p.set_pop_mask(pi, m)
     p.min_depth, p.max_depth, p.min_rmsQ, p.min_snpQ = 3, 255, 25, 25
     p.min_mapQ, p.min_baseQ, p.flag = 13, 13, 0
     for k, v in kw.items():

@@ -23,7 +23,7 @@ class OrcParams(C.Structure):
     _fields_ = [("n_samples", C.c_int32), ("n_pops", C.c_int32), ("pop_mask", C.c_uint64 * 64),
                 ("pop_n", C.c_int32 * 64), ("min_depth", C.c_int32), ("max_depth", C.c_int32),
                 ("min_rmsQ", C.c_int32), ("min_snpQ", C.c_int32), ("min_mapQ", C.c_int32),
-                ("min_baseQ", C.c_int32), ("flag", C.c_uint32)]
+                ("min_baseQ", C.c_int32), ("flag", C.c_uint32), ("pop_mask_hi", C.c_uint64 * 64)]
 
 
 class OrcCmd(C.Structure):
@@ -100,7 +100,7 @@ class Setup:
         p = OrcParams()
         p.n_samples, p.n_pops = self.sm.n, len(self.sm.pops)
         for i, (m, c) in enumerate(zip(self.masks, self.pop_n)):
-            p.pop_mask[i], p.pop_n[i] = m, c
+            p.pop_mask[i], p.pop_mask_hi[i], p.pop_n[i] = m & ((1 << 64) - 1), m >> 64, c
         p.min_depth, p.max_depth, p.min_rmsQ, p.min_snpQ = o.min_depth, o.max_depth, o.min_rmsQ, o.min_snpQ
         p.min_mapQ, p.min_baseQ, p.flag = o.min_mapQ & 0xFF, o.min_baseQ & 0xFF, o.flag
         return p
@@ -216,7 +216,8 @@ def oracle_params_from(pbg_params):
     p = OrcParams()
     p.n_samples, p.n_pops = pbg_params.n_samples, pbg_params.n_pops
     for i in range(pbg_params.n_pops):
-        p.pop_mask[i], p.pop_n[i] = pbg_params.pop_mask[i], pbg_params.pop_n[i]
+        p.pop_mask[i], p.pop_mask_hi[i] = pbg_params.pop_mask[i], pbg_params.pop_mask_hi[i]
+        p.pop_n[i] = pbg_params.pop_n[i]
     p.min_depth, p.max_depth = pbg_params.min_depth, pbg_params.max_depth
     p.min_rmsQ, p.min_snpQ = pbg_params.min_rmsQ, pbg_params.min_snpQ
     p.min_mapQ, p.min_baseQ, p.flag = pbg_params.min_mapQ, pbg_params.min_baseQ, pbg_params.flag
@@ -224,16 +225,17 @@ def oracle_params_from(pbg_params):
 
 
 def oracle_call(p, batch):
-    """orc_call_sites over a host batch -> (cb[L,n], types[L], fq[L], flags[L])."""
+    """orc_call_sites over a host batch -> (cb[L,n], types, fq[L], flags[L]); types is [L] u64
+    for n <= 64, [L, 2] (low, high word) beyond."""
     lib = oracle()
     L, n = batch["depth"].shape
     cb = np.zeros((L, n), np.uint64)
-    types = np.zeros(L, np.uint64)
+    types = np.zeros(L, np.uint64) if n <= 64 else np.zeros((L, 2), np.uint64)
     fq = np.zeros(L, np.int16)
     flags = np.zeros(L, np.uint8)
-    rd = batch["reads"] if len(batch["reads"]) else np.zeros(1, np.uint32)
-    assert lib.orc_call_sites(C.byref(p), L, np.ascontiguousarray(batch["ref"]).ctypes.data,
-                              np.ascontiguousarray(batch["depth"]).ctypes.data, np.ascontiguousarray(rd).ctypes.data,
+    rd = np.ascontiguousarray(batch["reads"] if len(batch["reads"]) else np.zeros(1, np.uint32))
+    ref, dep = np.ascontiguousarray(batch["ref"]), np.ascontiguousarray(batch["depth"])   # alive across the call
+    assert lib.orc_call_sites(C.byref(p), L, ref.ctypes.data, dep.ctypes.data, rd.ctypes.data,
                               cb.ctypes.data, types.ctypes.data, fq.ctypes.data, flags.ctypes.data) == 0
     return cb, types, fq, flags
 
@@ -244,9 +246,10 @@ def rows_from_oracle(types, flags, row_bytes):
     counted = (flags & 2) > 0
     seg = (flags & 4) > 0
     if row_bytes == 16:
+        lo, hi = (types[:, 0], types[:, 1]) if types.ndim == 2 else (types, np.zeros(L, np.uint64))
         out = np.zeros((L, 2), np.uint64)
-        out[:, 0] = np.where(counted, types, 0)
-        out[:, 1] = np.where(counted, (np.uint64(1) << np.uint64(62)) |
+        out[:, 0] = np.where(counted, lo, 0)
+        out[:, 1] = np.where(counted, hi | (np.uint64(1) << np.uint64(62)) |
                              np.where(seg, np.uint64(1) << np.uint64(63), np.uint64(0)), 0)
         return out.view(np.uint8).reshape(-1)
     W = row_bytes * 8
@@ -257,13 +260,16 @@ def rows_from_oracle(types, flags, row_bytes):
     return v.astype(dt).view(np.uint8)
 
 
-def rows_to_sites(rows_u8, row_bytes, n_sites):
-    """Unpack product rows -> (types u64, flags u8 with bit1 counted, bit2 seg)."""
+def rows_to_sites(rows_u8, row_bytes, n_sites, n=64):
+    """Unpack product rows -> (types, flags u8 with bit1 counted, bit2 seg); types as
+    oracle_call returns them for n samples."""
     if row_bytes == 16:
         w = rows_u8.view(np.uint64).reshape(n_sites, 2)
         types, hi = w[:, 0], w[:, 1]
         counted = (hi >> np.uint64(62)) & np.uint64(1)
         seg = (hi >> np.uint64(63)) & np.uint64(1)
+        if n > 64:
+            types = np.stack([types, hi & np.uint64(0x3FFFFFFFFFFFFFFF)], axis=1)
     else:
         dt = {2: np.uint16, 4: np.uint32, 8: np.uint64}[row_bytes]
         v = rows_u8.view(dt).astype(np.uint64)
@@ -273,3 +279,65 @@ def rows_to_sites(rows_u8, row_bytes, n_sites):
         types = v & ((np.uint64(1) << np.uint64(W - 2)) - np.uint64(1)) if W < 64 else v & np.uint64(0x3FFFFFFFFFFFFFFF)
     flags = (counted.astype(np.uint8) << 1) | (seg.astype(np.uint8) << 2)
     return types.astype(np.uint64), flags.astype(np.uint8)
+
+
+def select_samples(batch, order):
+    """A raw batch whose sample j is sample order[j] of `batch` (samples may repeat): the
+    per-position read runs are regrouped in the new sample order."""
+    dep = np.asarray(batch["depth"]).astype(np.int64)
+    L, n = dep.shape
+    start = (np.concatenate([[0], np.cumsum(dep.reshape(-1))])[:-1]).reshape(L, n)
+    sel = dep[:, order]
+    cnt = sel.reshape(-1)
+    st = start[:, order].reshape(-1)
+    seg = np.repeat(np.arange(cnt.size), cnt)
+    within = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    return {"ref": np.asarray(batch["ref"]), "depth": np.ascontiguousarray(sel, dtype=np.uint16),
+            "reads": np.ascontiguousarray(np.asarray(batch["reads"])[st[seg] + within], dtype=np.uint32)}
+
+
+class WideSetup(Setup):
+    """A golden case re-laid out for more than 64 samples (beyond the reference): its
+    populations keep their order and sample order, and an extra population of copies of the
+    first `n_copies` samples is inserted after population `after`, so the original populations
+    straddle both 64-bit words of the masks.  Copies pass / fail and carry alleles exactly as
+    their originals, so counted and segregating positions are unchanged; per-population
+    statistics of the original populations equal the reference's golden values (the checks
+    in test_wide_samples.py say which statistics are invariant and why)."""
+
+    def __init__(self, case_name, args, region, n_copies=32, after=1):
+        super().__init__(case_name, args, region)
+        sm0 = self.sm
+        order, samples, spop = [], [], []
+        pops = list(sm0.pops[:after + 1]) + ["copies"] + list(sm0.pops[after + 1:])
+        for p in range(len(sm0.pops)):
+            for s, sp in enumerate(sm0.sample_pop):
+                if sp == p:
+                    order.append(s)
+                    samples.append(sm0.samples[s])
+                    spop.append(p if p <= after else p + 1)
+            if p == after:
+                for s in range(n_copies):
+                    order.append(s)
+                    samples.append("x" + sm0.samples[s])
+                    spop.append(after + 1)
+        self.order = order
+        self.sm = opt.SampleModel(samples, pops, {}, spop)
+        self.masks, self.pop_n = self.sm.pop_masks()
+        if self.opts.flag & opt.BAM_OUTGROUP:
+            self.outidx = max(i for i, s in enumerate(self.sm.samples) if s == self.opts.outgroup)
+        self.batch = select_samples(self.batch, order)
+        self._kbatch = None
+
+
+def labelled_values(text):
+    """{(line, label[name]): value} plus {(line, '#k'): k-th leading field} of a TSV."""
+    out = {}
+    for li, line in enumerate(text.splitlines()):
+        f = line.split("\t")
+        for k in range(min(4, len(f))):
+            out[(li, f"#{k}")] = f[k]
+        for a, b in zip(f, f[1:]):
+            if a.endswith(":"):
+                out[(li, a)] = b
+    return out

@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
 def test_create_rejects_bad_params():
     lib = _lib.load()
     p = _lib.PbgParams()
-    p.n_samples, p.n_pops = 65, 1
+    p.n_samples, p.n_pops = _lib.PBG_MAX_SAMPLES + 1, 1
     h = C.c_void_p()
     assert lib.pbg_create(C.byref(h), 0, C.byref(p)) == _lib.PBG_E_ARG
     assert b"n_samples" in lib.pbg_last_error(None)

@@ -22,12 +22,13 @@ def _ctx(n, n_pops=2, **kw):
 
 # (samples, populations): every row width (2 / 4 / 8 / 16 bytes, both ends of each width)
 # and the r^2 table sizes that leave the LDS copy (2 x 13^3 > 4096 doubles at 24 samples)
-SHAPES = [(12, 2), (24, 2), (24, 3), (30, 3), (48, 2), (62, 2), (64, 4)]
+SHAPES = [(12, 2), (24, 2), (24, 3), (30, 3), (48, 2), (62, 2), (64, 4), (96, 3), (126, 2)]
 
 
 @pytest.mark.parametrize("n,kw,contig", [(12, {}, 0), (12, {}, 3), (24, {"flag": 0x02}, 0),
                                           (40, {"min_baseQ": 30, "min_mapQ": 61}, 1),
-                                          (64, {"max_depth": 12, "min_depth": 8}, 0), (5, {"max_depth": 300}, 2)])
+                                          (64, {"max_depth": 12, "min_depth": 8}, 0), (5, {"max_depth": 300}, 2),
+                                          (96, {}, 1)])
 def test_synthetic_generator_matches_oracle(gpu_lib, n, kw, contig):
     """pbg_synth_pileup = the oracle's raw generator + the host packer (call_base's per-read
     loop, libpopbam_feed.so), for every filter variant, k width and contig key."""
@@ -72,6 +73,8 @@ def test_synthetic_generator_matches_oracle(gpu_lib, n, kw, contig):
     (62, {}),                                   # 8-byte rows, widest single word
     (64, {"max_depth": 12, "min_depth": 8}),    # 16-byte rows, depth filters
     (12, {"flag": 0x20}),                       # BAM_HETEROZYGOTE: heterozygotes kept
+    (96, {}),                                   # two-word masks (beyond the reference's 64)
+    (126, {"min_snpQ": 40}),                    # the widest 16-byte row
 ])
 def test_call_kernel_matches_oracle(gpu_lib, n, kw):
     import torch
@@ -100,6 +103,8 @@ def test_call_kernel_matches_oracle(gpu_lib, n, kw):
     (40, {"min_baseQ": 30, "min_mapQ": 61}),    # k = 0 everywhere: never reference-only
     (64, {"max_depth": 12, "min_depth": 8}),
     (12, {"flag": 0x20}),
+    (96, {}),
+    (126, {}),
 ])
 def test_rows_only_call_matches_oracle(gpu_lib, n, kw):
     """Rows without consensus words (the statistics path): the kernel may then skip the
@@ -185,6 +190,8 @@ def test_window_stats_match_oracle(gpu_lib, n, npops, layout, stat, cmd_id, outp
     n_sites = 64 * 8000 if stat != 0x008 else 64 * 1600      # omega_max is O(S^3) on the oracle
     if n > 30:
         n_sites //= 2
+    if n > 64:
+        n_sites //= 2
     ctx, params = _ctx(n, npops)
     syn = workload.SynthPileup(ctx, n_sites, 10, SEED + n)
     if layout == "ref10kb":
@@ -199,14 +206,14 @@ def test_window_stats_match_oracle(gpu_lib, n, npops, layout, stat, cmd_id, outp
     hp.opts.jc = jc
     hp.step()
     torch.cuda.synchronize()
-    types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites)
+    types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites, n)
     gpu = _window_text(ctx, params, hp, cmd_id, output, wins, min_freq, jc)
     orc = _oracle_text(params, types, flags, cmd_id, output, wins, min_freq, jc)
     assert gpu == orc
     ctx.close()
 
 
-@pytest.mark.parametrize("n,npops", [(12, 2), (24, 3), (64, 4)])
+@pytest.mark.parametrize("n,npops", [(12, 2), (24, 3), (64, 4), (96, 3)])
 def test_u16_wrap_and_workspace_window(gpu_lib, n, npops):
     """One window over 1.28 M positions: ~25 k segregating sites (beyond LDS -> global
     workspace) and > 65535 differences per pair for some pairs at high theta."""
@@ -221,8 +228,8 @@ def test_u16_wrap_and_workspace_window(gpu_lib, n, npops):
         hp = workload.HotPath(ctx, syn, wins, stat)
         hp.step()
         torch.cuda.synchronize()
-        types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites)
-        assert int((flags & 4 > 0).sum()) > _lib.PBG_MAX_SAMPLES * 32
+        types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites, n)
+        assert int((flags & 4 > 0).sum()) > 64 * 32
         assert _window_text(ctx, params, hp, cmd_id, output, wins) == _oracle_text(params, types, flags, cmd_id,
                                                                                   output, wins)
     ctx.close()
@@ -296,7 +303,7 @@ def test_fixture_rows_only_and_cb_paths_match_oracle(gpu_lib, name):
 
 
 @pytest.mark.parametrize("n,npops,flag,outidx", [(12, 2, 0, 0), (24, 3, 0x40, 5), (64, 4, 0x40, 63), (11, 1, 0, 0),
-                                                 (30, 5, 0, 0)])
+                                                 (30, 5, 0, 0), (96, 3, 0x40, 90)])
 def test_sfs_bins_and_theta_w(gpu_lib, n, npops, flag, outidx):
     """The SFS bins, S and theta_W = S / a1[n_pop] (north_star outputs the reference never prints;
     parity unpinned) equal the oracle's calc_sfs integers, bit for bit, for every window layout,
@@ -314,7 +321,7 @@ def test_sfs_bins_and_theta_w(gpu_lib, n, npops, flag, outidx):
     hp.opts.outidx = outidx
     hp.step()
     ctx.sync_check()
-    types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites)
+    types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites, n)
     stride = ctx.sfs_stride
     nw = len(wins)
     bins = np.zeros(nw * npops * stride, np.int32)
