@@ -45,9 +45,11 @@ def parse():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xC0FFEE02)
     ap.add_argument("--cpu-sample", type=int, default=60_000, help="positions for the CPU port baseline (0 = skip all)")
     ap.add_argument("--ref-sample", type=int, default=200_000, help="positions for the reference-binary baseline")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
                     help="BASELINE.json configs[i]: 2 = 50 Msites x 12 samples (the metric's config), "
-                         "3 = whole genome 24 contigs x 125 Mbp x 24 samples, nucdiv+sfs+ld+diverge")
+                         "3 = whole genome 24 contigs x 125 Mbp x 24 samples, nucdiv+sfs+ld+diverge, "
+                         "4 = deep panel 200 Msites x 96 samples, 1 kb windows every 500 bp, nucdiv+sfs+haplo EHHS")
+    ap.add_argument("--step", type=int, default=500, help="config 4: window step (overlapping windows)")
     ap.add_argument("--contigs", type=int, default=24, help="config 3: contigs")
     ap.add_argument("--contig-len", type=int, default=125_000_000, help="config 3: positions per contig")
     ap.add_argument("--chunk", type=int, default=1 << 25, help="config 3: positions per streamed pileup chunk")
@@ -57,6 +59,18 @@ def parse():
             args.samples = 24
         if args.seed == 0xC0FFEE02:
             args.seed = 0xC0FFEE04
+    if args.config == 4:
+        if args.samples == 12:
+            args.samples = 96
+        if args.seed == 0xC0FFEE02:
+            args.seed = 0xC0FFEE05
+        if args.window == 10_000:
+            args.window = 1000
+        if args.contig_len == 125_000_000:
+            args.contig_len = 200_000_000
+        if args.chunk == 1 << 25:
+            args.chunk = 1 << 23   # 96 samples: ~16 GB of keys per chunk buffer
+        args.contigs = 1
     return args
 
 
@@ -80,6 +94,29 @@ def cpu_port(args):
     rd = np.ascontiguousarray(batch["reads"])
     tot = 0.0
     win = min(args.window, max(2, L // 4))
+    if args.config == 4:   # overlapping windows: the oracle's call + its window statistics over the list
+        step = args.step
+        wins = [(a, a + win) for a in range(0, L - win + 1, step)]
+        wb = np.array([a for a, _ in wins], np.int32)
+        we = np.array([b for _, b in wins], np.int32)
+        for cmd, out in ((4, 0), (6, 0), (1, 1)):   # nucdiv, sfs, haplo -o 1 (EHHS)
+            c = harness.OrcCmd()
+            c.cmd, c.output, c.min_sites, c.min_snps, c.min_freq = cmd, out, 10, 10, 1
+            c.chr_name = b"chr1"
+            c.sample_names = C.cast(sn, C.POINTER(C.c_char_p))
+            c.pop_names = C.cast(pn, C.POINTER(C.c_char_p))
+            t0 = time.perf_counter()
+            _, types, _, flags = harness.oracle_call(p, batch)
+            buf = C.create_string_buffer(1 << 24)
+            r = lib.orc_windows_from_sites(C.byref(p), C.byref(c), types.ctypes.data, flags.ctypes.data, len(wins),
+                                           wb.ctypes.data, we.ctypes.data, buf, 1 << 24)
+            tot += time.perf_counter() - t0
+            assert r >= 0
+        return {"value": round(L / tot / 1e6, 6), "unit": "Msites/s", "cores": 1, "kind": "port",
+                "sample": f"first {L} positions of the same synthetic pileup ({n} samples, depth {args.depth}); "
+                          f"oracle C++ restatement on 128-bit masks (the reference stops at 64 samples), nucdiv, sfs "
+                          f"and haplo EHHS as 3 separate passes (each re-calls all sites), {win} bp windows every "
+                          f"{step} bp; excludes BAM decode/pileup"}
     for cmd in (4, 6, 5):   # nucdiv, sfs, ld (popbam_func_t)
         c = harness.OrcCmd()
         c.cmd, c.output, c.min_sites, c.min_snps, c.min_freq = cmd, 0, 10, 10, 1
@@ -106,7 +143,7 @@ def cpu_baseline(args):
     (P = the host's CPU share, at most 16).  The oracle port's rate is reported beside it."""
     import ref_baseline
     port = cpu_port(args)
-    if not ref_baseline.available():
+    if args.config == 4 or not ref_baseline.available():   # the reference cannot hold 96 samples
         return port
     L, n = args.ref_sample, args.samples
     d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_{args.seed:x}_{L}_{n}", args.seed, L, n)
@@ -134,8 +171,12 @@ def bench_genome(args, torch, dist, world, rank):
     n = args.samples
     ctx = _lib.Context(workload.default_params(n), torch.cuda.current_device())
     lengths = [args.contig_len] * args.contigs
-    segs = genome.plan_genome(lengths, world, args.window)[rank]
-    stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS | _lib.PBG_S_DIV_IND
+    if args.config == 4:   # overlapping windows: contiguous window blocks per rank, halo included
+        segs = genome.plan_overlapping(args.contig_len, world, args.window, args.step)[rank]
+        stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_HAP_EHHS
+    else:
+        segs = genome.plan_genome(lengths, world, args.window)[rank]
+        stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS | _lib.PBG_S_DIV_IND
     gp = genome.GenomePass(ctx, segs, args.seed, args.depth, args.window, stats, args.chunk)
     for _ in range(args.warmup):
         gp.run()
@@ -177,9 +218,13 @@ def bench_genome(args, torch, dist, world, rank):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (counter-based pileup generated on device chunk by chunk, inside the timed region)",
-            "config": {"workload": f"configs[3]: synthetic whole genome {args.contigs} contigs x "
-                                   f"{args.contig_len / 1e6:g} Mbp x {n} samples, consensus call + nucdiv + sfs + "
-                                   f"ld(ZnS) + diverge, {args.window / 1e3:g} kb windows, sharded by contig",
+            "config": {"workload": (f"configs[3]: synthetic whole genome {args.contigs} contigs x "
+                                    f"{args.contig_len / 1e6:g} Mbp x {n} samples, consensus call + nucdiv + sfs + "
+                                    f"ld(ZnS) + diverge, {args.window / 1e3:g} kb windows, sharded by contig")
+                       if args.config == 3 else
+                       (f"configs[4]: synthetic deep panel {args.contig_len / 1e6:g} Msites x {n} samples, consensus "
+                        f"call + nucdiv + sfs + haplo EHHS, {args.window / 1e3:g} kb windows every {args.step} bp "
+                        f"(overlapping), window blocks per rank with a {args.window - args.step} bp halo"),
                        "genome_sites": total_sites, "sites_rank0": my_sites, "samples": n, "mean_depth": args.depth,
                        "window": args.window, "windows_rank0": gp.n_windows, "chunk_sites": args.chunk,
                        "chunks_rank0": chunks, "parallelism": f"dp{world} (contig-first shards, no collective)"},
@@ -213,7 +258,7 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    if args.config == 3:
+    if args.config in (3, 4):
         bench_genome(args, torch, dist, world, rank)
         if dist:
             dist.destroy_process_group()

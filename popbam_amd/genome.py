@@ -32,10 +32,16 @@ SITE_BLOCK = _lib.PBG_SITE_BLOCK
 
 @dataclass
 class Segment:
-    """Positions [beg, end) of contig `contig` (0-based), a whole number of windows."""
+    """Positions [beg, end) of contig `contig` (0-based), a whole number of windows.  With
+    step > 0 the windows are [a, a + win) for a in range(win_lo, win_hi, step) (overlapping
+    windows, BASELINE configs[4]; the reference has no step option) and [beg, end) includes
+    the halo the last of them reads."""
     contig: int
     beg: int
     end: int
+    step: int = 0
+    win_lo: int = 0
+    win_hi: int = 0
 
 
 def contig_windows(length: int, win: int, beg: int = 0, end: int | None = None):
@@ -69,6 +75,19 @@ def plan_genome(lengths: list[int], world: int, win: int) -> list[list[Segment]]
         load[r] += p.end - p.beg
     for r in range(world):
         plan[r].sort(key=lambda s: (s.contig, s.beg))
+    return plan
+
+
+def plan_overlapping(length: int, world: int, win: int, step: int) -> list[list[Segment]]:
+    """Overlapping windows [k*step, k*step + win) of one contig split into contiguous blocks of
+    windows, one per rank (each shard reads a halo of win - step positions)."""
+    nwin = max(0, (length - win) // step + 1)
+    plan = []
+    for r in range(world):
+        q, rem = divmod(nwin, world)
+        k0 = r * q + min(r, rem)
+        k1 = k0 + q + (1 if r < rem else 0)
+        plan.append([Segment(0, k0 * step, (k1 - 1) * step + win, step, k0 * step, k1 * step)] if k1 > k0 else [])
     return plan
 
 
@@ -116,7 +135,10 @@ class GenomePass:
         self.win_lists = []
         self.groups = []   # (first row byte, rows, window list)
         for si, s in enumerate(segments):
-            w = [(a - s.beg, b - s.beg) for a, b in contig_windows(s.end, win, s.beg, s.end)]
+            if s.step:
+                w = [(a - s.beg, a - s.beg + win) for a in range(s.win_lo, s.win_hi, s.step)]
+            else:
+                w = [(a - s.beg, b - s.beg) for a, b in contig_windows(s.end, win, s.beg, s.end)]
             self.win_lists.append(w)
             nrows_seg = (s.end - s.beg)
             if not self.groups or (self.row_base[si] - self.groups[-1][0]) // rb + nrows_seg >= (1 << 31) - 256:

@@ -69,3 +69,48 @@ def test_chunked_pass_equals_one_batch(gpu_lib, n, npops):
         tail = small.window_results(f)[-nw * per:]
         assert np.array_equal(tail.view(np.uint8), hp.out.t[f][:nw * per].cpu().numpy().view(np.uint8)), f
     ctx.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8, 13])
+@pytest.mark.parametrize("length,win,step", [(200_000_000, 1000, 500), (10_007, 1000, 500), (5_000, 700, 300),
+                                             (999, 1000, 500)])
+def test_overlapping_plan_covers_every_window_once(world, length, win, step):
+    """configs[4]'s overlapping windows: contiguous window blocks per rank, each segment holds
+    its windows entirely (the halo of win - step positions included), and every window
+    [k*step, k*step + win) of the contig lands on exactly one rank."""
+    plan = genome.plan_overlapping(length, world, win, step)
+    assert len(plan) == world
+    got = []
+    for segs in plan:
+        for s in segs:
+            ws = list(range(s.win_lo, s.win_hi, s.step))
+            assert ws and s.beg == ws[0] and s.end == ws[-1] + win <= length
+            got += ws
+    want = list(range(0, length - win + 1, step)) if length >= win else []
+    assert got == want
+
+
+@pytest.mark.gpu
+def test_overlapping_pass_matches_one_batch(gpu_lib):
+    """96 samples, overlapping 1 kb windows every 500 bp, nucdiv + sfs + haplo EHHS: the chunked
+    pass over a two-rank plan equals one batch of the whole contig through the hot path."""
+    from popbam_amd import _lib
+    n, L, win, step = 96, 400_000, 1000, 500
+    ctx = _lib.Context(workload.default_params(n, 2), 0)
+    stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_HAP_EHHS
+    parts = []
+    for segs in genome.plan_overlapping(L, 2, win, step):
+        gp = genome.GenomePass(ctx, segs, SEED, 10, win, stats, chunk=64 * 1000)
+        gp.run()
+        gp.synchronize()
+        parts.append(gp)
+    syn = workload.SynthPileup(ctx, L, 10, SEED, contig=0, pos0=0)
+    wins = [(a, a + win) for a in range(0, L - win + 1, step)]
+    hp = workload.HotPath(ctx, syn, wins, stats)
+    hp.step()
+    ctx.sync_check()
+    for f in workload.HotPath.fields_for(stats):
+        x = np.concatenate([p.window_results(f) for p in parts])
+        assert np.array_equal(x.view(np.uint8), hp.out.t[f].cpu().numpy().view(np.uint8)), f
+    assert (hp.out.t["segsites"].cpu().numpy() > 0).mean() > 0.5
+    ctx.close()
