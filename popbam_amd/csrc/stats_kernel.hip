@@ -50,6 +50,10 @@ template <>
 __device__ __forceinline__ uint64_t pop_mask<uint64_t>(const DevParams &P, int i) { return P.pop_mask[i]; }
 template <>
 __device__ __forceinline__ M2 pop_mask<M2>(const DevParams &P, int i) { return {P.pop_mask[i], P.pop_mask_hi[i]}; }
+__device__ __forceinline__ uint64_t shfl_xor_mask(uint64_t x, int o) {
+    return ((uint64_t)(uint32_t)__shfl_xor((int)(x >> 32), o, 64) << 32) | (uint32_t)__shfl_xor((int)x, o, 64);
+}
+__device__ __forceinline__ M2 shfl_xor_mask(M2 x, int o) { return {shfl_xor_mask(x.lo, o), shfl_xor_mask(x.hi, o)}; }
 template <int RB>
 struct RowMask { using T = uint64_t; };
 template <>
@@ -116,8 +120,9 @@ WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_to
     L.diff = take(diff ? (uint32_t)(n * n * 2) : 0);
     L.acc = take((stats & (PBG_S_NUCDIV | PBG_S_HAP_DXY)) ? (uint32_t)(np * np * 4) : 0);
     L.amin = take((stats & PBG_S_HAP_DXY) ? (uint32_t)(np * np * 4) : 0);
-    L.bins = take((stats & (PBG_S_SFS | PBG_S_DIV_POP | PBG_S_HAP_K | PBG_S_HAP_EHHS)) ? (uint32_t)(np * (sfs_stride + 2) * 4)
-                                                                                       : 0);
+    L.bins = take((stats & (PBG_S_SFS | PBG_S_DIV_POP | PBG_S_HAP_K | PBG_S_HAP_EHHS))
+                      ? (uint32_t)((np + 1) * (sfs_stride + 2) * 4)   // + one scratch slice (haplo histogram)
+                      : 0);
     L.rbuf = take((stats & PBG_S_ZNS) ? (uint32_t)np * 4 : 0);   // ZnS: variable sites per population
     L.r2lds = 0;                                                   // (r^2 tables: window_zns_kernel)
     L.r2 = take(0);
@@ -478,48 +483,68 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         }
     }
 
-    // ---- haplo K / Kdiv and EHHS (lane per population)
+    // ---- haplo K / Kdiv and EHHS: one population at a time, lanes over its samples / sites
     if (stats & (PBG_S_HAP_K | PBG_S_HAP_EHHS))
-        for (int i = lane; i < np; i += 64) {
+        for (int i = 0; i < np; ++i) {
             const int nelem = P.pop_n[i];
-            int nh = 0;
-            double hdiv;
-            int32_t *b = s_bins + i * bstride;   // sample ids of the population (<= sfs_stride - 1)
+            int nh = 1;
+            double hdiv = 1.0;
+            int32_t *b = s_bins + i * bstride;    // sample ids of the population (<= sfs_stride - 1)
+            int32_t *hist = s_bins + np * bstride;   // scratch slice after the populations'
             if (nelem > 1) {
-                int c = 0;
-                for (int j = 0; j < n; j++)
-                    if (P.sample_pop[j] == i) b[c++] = j;
-                // local indices j,k index the global diff matrix (A.11)
-                for (int j = 0; j < nelem - 1; j++)
-                    for (int k = j + 1; k < nelem; k++)
-                        if (s_diff[j * n + k] == 0 && b[k] > b[j]) b[k] = j;
-                int ff = 0;
-                for (int j = 0; j < nelem; j++) {
-                    int f = 0;
-                    for (int q = 0; q < nelem; q++) f += b[q] == j;
-                    if (f > 0) ++nh;
-                    ff += f * f;
+                // b[c] = global id of the population's c-th sample (ordered compaction)
+                int base = 0;
+                for (int v0 = 0; v0 < n; v0 += 64) {
+                    const int v = v0 + lane;
+                    const bool in = v < n && P.sample_pop[v] == i;
+                    const uint64_t m = __ballot(in);
+                    if (in) b[base + (int)__popcll(m & ((1ULL << lane) - 1))] = v;
+                    base += (int)__popcll(m);
                 }
+                for (int j = lane; j < nelem; j += 64) hist[j] = 0;
+                __syncthreads();
+                // calc_nhaps's merge loop (pop_haplo.cpp:221-231), local indices j, k into the
+                // global diff matrix (A.11).  Step j only reads b[j], final once steps < j are
+                // done, and each b[k], k > j: the k's of one step run across lanes.
+                for (int j = 0; j < nelem - 1; j++) {
+                    const int bj = b[j];
+                    for (int k = j + 1 + lane; k < nelem; k += 64)
+                        if (s_diff[j * n + k] == 0 && b[k] > bj) b[k] = j;
+                    __syncthreads();
+                }
+                // f_j = #{q : b[q] == j}, j < nelem: an LDS histogram
+                for (int q = lane; q < nelem; q += 64)
+                    if (b[q] >= 0 && b[q] < nelem) atomicAdd(&hist[b[q]], 1);
+                __syncthreads();
+                int my_nh = 0, my_ff = 0;
+                for (int j = lane; j < nelem; j += 64) {
+                    const int f = hist[j];
+                    my_nh += f > 0 ? 1 : 0;
+                    my_ff += f * f;
+                }
+                nh = wave_sum(my_nh);
+                const int ff = wave_sum(my_ff);
                 const double sh = (double)(ff) / (double)(nelem * nelem);
                 hdiv = 1.0 - ((1.0 - sh) * (double)(nelem / (nelem - 1)));
-            } else {
-                nh = 1;
-                hdiv = 1.0;
+                __syncthreads();   // hist / b reused by the next population
             }
             if (stats & PBG_S_HAP_K) {
-                if (O.nhaps) O.nhaps[(size_t)w * np + i] = nh;
-                if (O.hap_val) O.hap_val[(size_t)w * np + i] = x86nan(1.0 - hdiv);
+                if (lane == 0) {
+                    if (O.nhaps) O.nhaps[(size_t)w * np + i] = nh;
+                    if (O.hap_val) O.hap_val[(size_t)w * np + i] = x86nan(1.0 - hdiv);
+                }
             } else {
                 double e;
                 if (nelem < 4) {
                     e = __longlong_as_double(0x7FF8000000000000LL);
                 } else {
                     // max multiplicity among non-singleton partitions, ties -> smallest value
-                    // (std::list sort + unique + remove, pop_haplo.cpp:273-313)
+                    // (std::list sort + unique + remove, pop_haplo.cpp:273-313): lanes over the
+                    // candidate sites, then a (count desc, value asc) reduction across lanes
                     const M pm = pop_mask<M>(P, i);
                     int best = 0;
                     M max_site{};
-                    for (uint32_t j = 0; j < S; j++) {
+                    for (uint32_t j = (uint32_t)lane; j < S; j += 64) {
                         const M pt = seg_at(j) & pm;
                         const unsigned f = pc(pt);
                         if (!(f > 1 && (int)f < nelem - 1)) continue;
@@ -531,13 +556,21 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                             max_site = pt;
                         }
                     }
+                    for (int o = 32; o > 0; o >>= 1) {
+                        const int ob = __shfl_xor(best, o, 64);
+                        const M os = shfl_xor_mask(max_site, o);
+                        if (ob > best || (ob == best && os < max_site)) {
+                            best = ob;
+                            max_site = os;
+                        }
+                    }
                     const unsigned popf = pc(max_site);
                     const int pn = nelem;
                     const double sh = (1.0 - ((double)((int)(popf * popf) + ((pn - (int)popf) * (pn - (int)popf))) / (pn * pn))) *
                                       (double)(pn / (pn - 1));
                     e = hdiv / (1.0 - sh);
                 }
-                if (O.hap_val) O.hap_val[(size_t)w * np + i] = e;
+                if (lane == 0 && O.hap_val) O.hap_val[(size_t)w * np + i] = e;
             }
         }
     (void)s_misc;
