@@ -162,6 +162,30 @@ def cpu_baseline(args):
     return out
 
 
+def pcie_rate(torch, batch_bytes: int, step_s: float, sites: int) -> dict:
+    """The host-buffer boundary (pbg_run / the CLI hand the batch over in host memory): measured
+    pinned host -> device bandwidth, and the rate the hot path would reach with the batch's
+    bytes crossing PCIe, serially (copy, then call + stats) and double-buffered (copy of batch
+    i+1 under the compute of batch i).  Never `value`: that is with the input resident."""
+    n = 1 << 30
+    h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(4):
+        d.copy_(h, non_blocking=True)
+    e1.record()
+    torch.cuda.synchronize()
+    gbps = 4 * n / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    copy_s = batch_bytes / (gbps * 1e9)
+    del h, d
+    return {"h2d_GBps": round(gbps, 2), "batch_bytes": batch_bytes, "copy_ms": round(copy_s * 1e3, 2),
+            "Msites_per_s_serial": round(sites / (copy_s + step_s) / 1e6, 2),
+            "Msites_per_s_overlapped": round(sites / max(copy_s, step_s) / 1e6, 2)}
+
+
 def bench_genome(args, torch, dist, world, rank):
     """configs[3]: the whole synthetic genome (contigs x contig-len, 24 samples) streamed through
     HBM in double-buffered pileup chunks (popbam_amd.genome), contig-first shards across ranks,
@@ -361,6 +385,8 @@ def main():
                              "GBps": round(stats_bytes / (stats_ms * 1e-3) / 1e9, 2),
                              "Msites_per_s_stats_only": round(args.sites / (stats_ms * 1e-3) / 1e6, 2)},
         }
+        if world == 1:
+            out["pcie_inclusive"] = pcie_rate(torch, layout_bytes - args.sites * n, elapsed / args.steps, args.sites)
         if world == 1 and args.cpu_sample > 0:
             out["cpu_baseline"] = cpu_baseline(args)
         else:
