@@ -795,6 +795,114 @@ __global__ __launch_bounds__(64) void window_zns_kernel(DevParams P, DevTables T
     }
 }
 
+// ZnS sums, 16 lanes per chain: each 16-lane row of a wave owns one (window, population)
+// chain; per step its lanes compute the r^2 of the next 16 pairs of the current row a (lanes
+// past the row's end give +0.0) and every lane of the row adds the 16 values in pair order
+// (DPP row_newbcast hands lane j's value to the whole row), so the chain is the reference's
+// exact sequence of additions with 16-wide r^2 work.  Four chains per wave, 16 per workgroup,
+// and four times the waves of the quad kernel above: the dependent adds of more chains
+// interleave on each SIMD.
+template <int J>
+__device__ __forceinline__ double row_bcast(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x150 + J, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x150 + J, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+template <int J>
+__device__ __forceinline__ void add_row(double &acc, double r) {
+    if constexpr (J < 16) {
+        acc += row_bcast<J>(r);
+        add_row<J + 1>(acc, r);
+    }
+}
+constexpr int kZnsRowUnroll = 2;
+template <class M>
+__global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A,
+                                                             int r2_lds) {
+    constexpr int kStage = zns_stage<M>(), kStride = zns_stride<M>();
+    extern __shared__ __align__(16) double s_dyn[];
+    __shared__ __align__(16) double s_val[16][16 * kZnsRowUnroll];             // a step's r^2 per chain
+    double *s_r2t = s_dyn;                                                      // [r2_lds]
+    M *s_t = reinterpret_cast<M *>(s_dyn + r2_lds);                            // [16][kStride] masks
+    for (int i = threadIdx.x; i < r2_lds; i += 256) s_r2t[i] = T.r2[i];
+    const int np = P.npops;
+    const int lane = threadIdx.x & 63, g = lane & 15, q = (int)(threadIdx.x >> 4);   // q: chain slot 0..15
+    double *sv = s_val[q];
+    const uint32_t nch = n_win * (uint32_t)np;
+    const uint32_t ch = blockIdx.x * 16 + (uint32_t)q;
+    int V = 0;
+    const M *L = reinterpret_cast<const M *>(A.pool);
+    int np1 = 1, r2o = 0;
+    if (ch < nch) {
+        const uint32_t w = ch / (uint32_t)np;
+        const int i = (int)(ch - w * (uint32_t)np);
+        V = A.var_count[ch];
+        L = reinterpret_cast<const M *>(A.pool + A.zoff[ch]);
+        np1 = P.pop_n[i] + 1;
+        r2o = T.r2_off[i];
+    }
+    // the wave's four chains staged in LDS, or all read from the pool (wave-uniform)
+    const bool staged = !__ballot(V > kStage);
+    M *lt = s_t + q * kStride;
+    if (staged)
+        for (int j = g; j < V; j += 16) lt[j] = L[j];
+    __syncthreads();
+    auto run = [&](const M *lst, const double *r2p) -> double {
+        const int vm1 = V > 0 ? V - 1 : 0;
+        int a = 0, b0 = 1;
+        double acc = 0.0;
+        while (__ballot(a < V - 1)) {   // wave-uniform: until the wave's four chains are done
+            double r[kZnsRowUnroll];
+#pragma unroll
+            for (int u = 0; u < kZnsRowUnroll; ++u) {
+                const int b = b0 + g;
+                const bool ok = (a < V - 1) & (b < V);
+                const M ta = lst[min(a, vm1)], tb = lst[min(b, vm1)];
+                const double rv = r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
+                r[u] = ok ? rv : 0.0;
+                b0 += 16;
+                const bool nxt = (b0 >= V) & (a < V - 1);
+                a += nxt ? 1 : 0;
+                b0 = nxt ? a + 1 : b0;
+            }
+#ifdef PBG_ZNS_DPP
+#pragma unroll
+            for (int u = 0; u < kZnsRowUnroll; ++u) add_row<0>(acc, r[u]);   // pair order: lane 0..15
+#else
+            // the row's values through LDS: every lane of the row reads the same words (broadcast
+            // reads, two doubles each) and adds them in pair order
+#pragma unroll
+            for (int u = 0; u < kZnsRowUnroll; ++u) sv[16 * u + g] = r[u];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const double2 *sv2 = reinterpret_cast<const double2 *>(sv);
+#pragma unroll
+            for (int x = 0; x < 8 * kZnsRowUnroll; ++x) {
+                const double2 v = sv2[x];
+                acc += v.x;
+                acc += v.y;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#endif
+        }
+        return acc;
+    };
+    double acc;
+    if (staged) acc = r2_lds ? run(lt, s_r2t + r2o) : run(lt, T.r2 + r2o);
+    else acc = r2_lds ? run(L, s_r2t + r2o) : run(L, T.r2 + r2o);
+    if (g == 0 && ch < nch) {
+        const uint32_t w = ch / (uint32_t)np;
+        double val = 0.0;
+        if (A.seg_count[w] >= 1) {
+            const int ns = A.ld_ns[ch];
+            val = acc * (2.0 / (ns * (ns - 1)));
+        }
+        if (A.out.ld_val) A.out.ld_val[ch] = x86nan(val);
+    }
+}
+
 template __global__ void window_stats_kernel<2>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
 template __global__ void window_stats_kernel<4>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
 template __global__ void window_stats_kernel<8>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
@@ -817,12 +925,21 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
         const int r2_lds = r2_total <= 4608 ? r2_total : 0;   // <= 36 KB of LDS per wave
         const uint32_t chains = n_win * (uint32_t)P.npops;
         const dim3 g((chains + 15) / 16);
+#ifdef PBG_ZNS_QUAD
         if (rb == 16)
             hipLaunchKernelGGL(window_zns_kernel<M2>, g, dim3(64), (size_t)r2_lds * 8 + 16 * zns_stride<M2>() * 16, stream,
                                P, T, n_win, A, r2_lds);
         else
             hipLaunchKernelGGL(window_zns_kernel<uint64_t>, g, dim3(64), (size_t)r2_lds * 8 + 16 * zns_stride<uint64_t>() * 8,
                                stream, P, T, n_win, A, r2_lds);
+#else
+        if (rb == 16)
+            hipLaunchKernelGGL(window_zns_row_kernel<M2>, g, dim3(256), (size_t)r2_lds * 8 + 16 * zns_stride<M2>() * 16,
+                               stream, P, T, n_win, A, r2_lds);
+        else
+            hipLaunchKernelGGL(window_zns_row_kernel<uint64_t>, g, dim3(256),
+                               (size_t)r2_lds * 8 + 16 * zns_stride<uint64_t>() * 8, stream, P, T, n_win, A, r2_lds);
+#endif
     }
     const uint32_t ld = A.stats & (PBG_S_OMEGA | PBG_S_WALL);
     if (ld) {
