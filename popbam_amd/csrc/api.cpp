@@ -72,6 +72,25 @@ int fail(pbg_ctx *c, int code, const std::string &msg) {
             return fail((ctx), PBG_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
     } while (0)
 
+// rms of call_base (popbam.cpp:292) for k keys with sum mapQ^2 = rmsq: the reference's float
+// division, sqrtf and (unsigned long long)(x + 0.499)
+uint32_t rms_of(uint32_t rmsq, int k) {
+    const float f = (float)rmsq / (float)k;
+    return (uint32_t)((double)std::sqrt(f) + 0.499);
+}
+// smallest sum mapQ^2 (mapQ <= 255) whose rms passes qfilter with k keys, or ~0 when none does
+uint32_t rms_threshold(int k, int min_rmsQ, int min_depth, int max_depth) {
+    if (k < 1 || k < min_depth || k > max_depth) return 0xFFFFFFFFu;
+    uint32_t lo = 0, hi = (uint32_t)k * 65025u;   // rms is monotone in rmsq
+    if ((int)rms_of(hi, k) < min_rmsQ) return 0xFFFFFFFFu;
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if ((int)rms_of(mid, k) >= min_rmsQ) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
 int row_bytes_for(int n) { return n <= 14 ? 2 : n <= 30 ? 4 : n <= 62 ? 8 : 16; }
 
 template <class T>
@@ -148,6 +167,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
                 }
                 d.sample_pop[v] = (int8_t)i;
             }
+    for (int k = 0; k <= 16; ++k) d.rms_thr[k] = rms_threshold(k, p->min_rmsQ, p->min_depth, p->max_depth);
     d.sfs_stride = 1;
     for (int i = 0; i < p->n_pops; ++i) d.sfs_stride = std::max(d.sfs_stride, p->pop_n[i] + 1);
     auto bad = [&](hipError_t e, const char *what) {

@@ -23,6 +23,11 @@ struct DevParams {
     int32_t k16;          // k[] is u16 (max_depth > 255), else u8
     int32_t sfs_stride;   // largest population + 1 (pbg_window_out.sfs_bins row)
     int8_t sample_pop[PBG_MAX_SAMPLES];   // population of each sample (-1: none); masks are disjoint
+    // qfilter of a reference-only sample with k = d keys (call_scan_kernel): it passes iff
+    // sum mapQ^2 >= rms_thr[d].  rms = (unsigned)(sqrtf((float)rmsq / d) + 0.499) is monotone in
+    // rmsq, so "rms >= min_rmsQ && min_depth <= d <= max_depth" is one threshold per d, found on
+    // the host with the same IEEE float division and square root (rms_threshold, api.cpp).
+    uint32_t rms_thr[17];
 };
 
 // Host-built tables resident in HBM for the lifetime of a context.
