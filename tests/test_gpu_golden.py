@@ -21,3 +21,16 @@ def test_gpu_matches_reference(gpu_lib, name, idx):
     oob = harness.snp_oob_cells(harness.oracle_run(st)) if cs["args"][0] == "snp" else None
     ok, diff = harness.same_output(cs["args"], gold, ours, oob)
     assert ok, f"{cs['args']} {cs['region']}\n gold: {diff[0]}\n ours: {diff[1]}"
+
+
+@pytest.mark.gpu
+def test_ms_header_needs_a_window(gpu_lib):
+    """snp -o 2 prints its header inside the window loop at cw == 0 (pop_snp.cpp:114-115): a
+    region shorter than one window prints nothing at all (oracle and GPU agree; no golden case
+    can hold an empty output, parity pinned by the reference's loop structure)."""
+    st = harness.Setup("g13_snpformats", ["snp", "-o", "2", "-w", "2"], "chr1:1-1500")
+    assert harness.oracle_run(st) == ""
+    assert engine.run_command(st.opts, st.sm, st.chr, st.beg, st.end, st.kbatch, refid=st.refid) == ""
+    st = harness.Setup("g13_snpformats", ["snp", "-o", "2", "-w", "2"], "chr1:1-2001")   # one window: header
+    ours = engine.run_command(st.opts, st.sm, st.chr, st.beg, st.end, st.kbatch, refid=st.refid)
+    assert ours.startswith("ms ") and ours == harness.oracle_run(st)
