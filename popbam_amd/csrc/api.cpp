@@ -53,6 +53,9 @@ struct pbg_ctx {
     size_t synth_cap = 0;
     // pbg_run text kept when the caller's buffer was too small (pbg_take_text)
     std::string text;
+    // second stream for the deep-task queue kernel beside the shallow one (pbg_call_sites)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_scan = nullptr, ev_deep = nullptr;
 };
 
 namespace {
@@ -229,6 +232,12 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
 void pbg_destroy(pbg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->aux) {
+        (void)hipStreamSynchronize(c->aux);
+        (void)hipStreamDestroy(c->aux);
+        (void)hipEventDestroy(c->ev_scan);
+        (void)hipEventDestroy(c->ev_deep);
+    }
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
                     (void *)c->d_fbeta, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
@@ -314,9 +323,14 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         ++c->ev_used;
         HIPCHK(c, hipEventRecord(c0, (hipStream_t)stream));
     }
+    if (!c->aux) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_deep, hipEventDisableTiming));
+    }
     const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys};
     HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, B, cap, rows, cb, c->d_err, c->deep,
-                                     (hipStream_t)stream, e0, e1));
+                                     (hipStream_t)stream, e0, e1, c->aux, c->ev_scan, c->ev_deep));
     if (c1) HIPCHK(c, hipEventRecord(c1, (hipStream_t)stream));
     return PBG_OK;
 }

@@ -184,9 +184,13 @@ struct Batch {
 };
 
 // kernel launchers (defined in call_kernel.hip / stats_kernel.hip)
+// aux (may be null): a second stream the deep-task queue kernel runs on, beside the shallow
+// one (they read disjoint queue ends); ev_scan / ev_deep order it after the scan and the fold
+// after it.
 hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, const Batch &B, uint32_t cap,
                              void *rows, uint64_t *cb, int *err, const struct DeepBufs &D, hipStream_t stream,
-                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, hipStream_t aux = nullptr,
+                             hipEvent_t ev_scan = nullptr, hipEvent_t ev_deep = nullptr);
 size_t call_sites_lds_bytes(int n, uint32_t cap);
 // synthetic batch: k / rmsq / ref + per-block key totals, then an exclusive scan of the totals
 // into block_off (scratch: one u64 per 1024 blocks), then the keys
