@@ -177,11 +177,21 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         return q;
     };
     // seg rows of word c (in window): bit mask + types; `store` gets (index, types)
+    // the window's 16-byte words in groups of kLoadAhead per lane: a group's loads are issued
+    // together, so the dependent compaction steps wait on one memory latency per group
+    constexpr int kLoadAhead = 4;
     auto compact = [&](M *dst, uint32_t cap, bool count_sites, int &my_counted) -> uint32_t {
         uint32_t S = 0;
-        for (int64_t cb = c0; cb < c1; cb += 64) {
+        uint4 qa[kLoadAhead];
+        for (int64_t cg = c0; cg < c1; cg += 64 * kLoadAhead) {
+#pragma unroll
+        for (int u = 0; u < kLoadAhead; ++u) qa[u] = load_word(cg + 64 * u + lane);
+#pragma unroll
+        for (int u = 0; u < kLoadAhead; ++u) {
+            const int64_t cb = cg + 64 * u;
+            if (cb >= c1) break;   // wave-uniform
             const int64_t c = cb + lane;
-            const uint4 q = load_word(c);
+            const uint4 q = qa[u];
             M t[R];
             uint32_t segm = 0;
 #pragma unroll
@@ -203,6 +213,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                     ++j;
                 }
             S += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
         }
         return S;
     };
@@ -821,7 +832,8 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
                                                              int r2_lds) {
     constexpr int kStage = zns_stage<M>(), kStride = zns_stride<M>();
     extern __shared__ __align__(16) double s_dyn[];
-    __shared__ __align__(16) double s_val[16][16 * kZnsRowUnroll];             // a step's r^2 per chain
+    // a step's r^2 per chain; +2 doubles per chain so the four rows of a wave read different banks
+    __shared__ __align__(16) double s_val[16][16 * kZnsRowUnroll + 2];
     double *s_r2t = s_dyn;                                                      // [r2_lds]
     M *s_t = reinterpret_cast<M *>(s_dyn + r2_lds);                            // [16][kStride] masks
     for (int i = threadIdx.x; i < r2_lds; i += 256) s_r2t[i] = T.r2[i];
