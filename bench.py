@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--contigs", type=int, default=24, help="config 3: contigs")
     ap.add_argument("--contig-len", type=int, default=125_000_000, help="config 3: positions per contig")
     ap.add_argument("--chunk", type=int, default=1 << 25, help="config 3: positions per streamed pileup chunk")
+    ap.add_argument("--pieces", type=int, default=1,
+                    help="config 2: the contig's call in this many pieces (window borders), each piece's "
+                         "statistics on a second stream beside the next piece's call (1 = call, then statistics)")
     args = ap.parse_args()
     if args.config == 3:
         if args.samples == 12:
@@ -299,13 +302,19 @@ def main():
     stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS
     hp = workload.HotPath(ctx, syn, wins, stats)
     stream = torch.cuda.current_stream()
+    stats_stream = torch.cuda.Stream()
+    pts = hp.pipeline(args.pieces) if args.pieces > 1 else [0, args.sites]
+
+    def step():
+        if args.pieces > 1:
+            hp.step_pipelined(stream, stats_stream)
+        else:
+            hp.step(stream)
 
     for _ in range(args.warmup):
-        hp.step(stream)
+        step()
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     # HIP events around the dominant kernel (call_scan_kernel), recorded by the library on the
     # stream it launches on (torch's events only bracket whole stages)
     ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 1), "pbg_set_kernel_timing")
@@ -313,12 +322,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for e0, e1, e2 in ev:
-        e0.record(stream)
-        hp.call(stream)
-        e1.record(stream)
-        hp.window_stats(stream)
-        e2.record(stream)
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -327,21 +332,34 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
-    call_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
-    stats_ms = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
     kt, kn = C.c_double(0.0), C.c_uint32(0)
     ctx.check(ctx.lib.pbg_kernel_time(ctx.h, C.byref(kt), C.byref(kn)), "pbg_kernel_time")
-    scan_ms = kt.value / max(1, kn.value)
-    total_sites = args.sites * world * args.steps
-    value = total_sites / elapsed / 1e6
     ct, cn = C.c_double(0.0), C.c_uint32(0)
     ctx.check(ctx.lib.pbg_call_time(ctx.h, C.byref(ct), C.byref(cn)), "pbg_call_time")
-    call_lib_ms = ct.value / max(1, cn.value)
+    ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
+
+    # stage breakdown (untimed for `value`): the call of every piece, then the statistics of
+    # every piece, serially on one stream (the same launches as the timed steps)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+    for e0, e1, e2 in ev:
+        e0.record(stream)
+        hp.call_pieces(stream) if args.pieces > 1 else hp.call(stream)
+        e1.record(stream)
+        hp.stats_pieces(stream) if args.pieces > 1 else hp.window_stats(stream)
+        e2.record(stream)
+    torch.cuda.synchronize()
+    call_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
+    stats_ms = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
+    scan_ms = kt.value / max(1, kn.value)            # per call_scan_kernel launch (one per piece)
+    total_sites = args.sites * world * args.steps
+    value = total_sites / elapsed / 1e6
+    call_lib_ms = ct.value / max(1, args.steps)      # whole call stage per step (all pieces)
     call_bytes = syn.survey_bytes()          # sum(2k + 5) + 1 + row_bytes per position
     scan_bytes = call_bytes
     layout_bytes = syn.layout_bytes_scan()
-    achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
+    scan_bytes_launch = scan_bytes * args.steps // max(1, kn.value)   # per launch (the pieces' mean)
+    achieved = scan_bytes * args.steps / (kt.value * 1e-3) / 1e9
     stats_bytes = args.sites * ctx.row_bytes
 
     # per-launch HBM traffic from rocprofv3 PMC counters, when a profile of this code is committed
@@ -352,7 +370,7 @@ def main():
             with open(pmc) as f:
                 d = json.load(f)
             if (d.get("sites") == args.sites and d.get("samples") == n and d.get("depth") == args.depth
-                    and d.get("layout") == LAYOUT):
+                    and d.get("layout") == LAYOUT and d.get("pieces", 1) == len(pts) - 1):
                 traffic = d.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -370,18 +388,19 @@ def main():
                                     f"consensus call + nucdiv + sfs + ld(ZnS), {args.window / 1e3:g} kb windows"),
                        "sites_per_gpu": args.sites, "samples": n, "mean_depth": args.depth,
                        "window": args.window, "windows_per_gpu": len(wins), "keys_per_gpu": syn.n_keys,
-                       "parallelism": f"dp{world} (independent window-range shards, no collective)"},
+                       "parallelism": f"dp{world} (independent window-range shards, no collective)",
+                       "pieces": len(pts) - 1},
             "roofline": {"bound": "hbm", "kernel": "call_scan_kernel", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "bytes_per_launch": scan_bytes, "ms_per_launch": round(scan_ms, 4),
+                         "traffic": traffic, "bytes_per_launch": scan_bytes_launch, "ms_per_launch": round(scan_ms, 4),
                          "bytes_basis": "SURVEY 8(d): sum over (position, sample) of 2k+5, +1 +row_bytes per position",
                          "layout_bytes_per_launch": layout_bytes,
-                         "frac_layout": round(layout_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-            "call_stage": {"ms_per_step": round(call_ms, 4), "ms_library_events": round(call_lib_ms, 4),
+                         "frac_layout": round(layout_bytes * args.steps / (kt.value * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "call_stage": {"ms_serial": round(call_ms, 4), "ms_library_events": round(call_lib_ms, 4),
                            "bytes": call_bytes, "GBps": round(call_bytes / (call_lib_ms * 1e-3) / 1e9, 2),
                            "frac": round(call_bytes / (call_lib_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "kernels": "call_scan + call_slow + call_deepq + call_overflow + call_fold"},
-            "window_stats": {"ms_per_launch": round(stats_ms, 4), "rows_bytes": stats_bytes,
+            "window_stats": {"ms_serial": round(stats_ms, 4), "rows_bytes": stats_bytes,
                              "GBps": round(stats_bytes / (stats_ms * 1e-3) / 1e9, 2),
                              "Msites_per_s_stats_only": round(args.sites / (stats_ms * 1e-3) / 1e6, 2)},
         }

@@ -25,6 +25,7 @@ struct pbg_ctx {
     int row_bytes = 8;
     double *d_fk = nullptr, *d_beta = nullptr, *d_lhet = nullptr, *d_sfs = nullptr, *d_r2 = nullptr;
     double *d_fbeta = nullptr;
+    double *d_lb = nullptr;
     int *d_err = nullptr;
     std::string err;
     // per-pileup LDS staging capacity (keyed by block_off pointer and size), so repeated
@@ -195,6 +196,16 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
                         // the register path relies on it for its zero padding words
                         fbeta[pbg::fbeta_index(q, nn, cc, w)] = q ? fk[w] * beta[q << 16 | nn << 8 | cc] : 0.0;
         if ((e = upload(&c->d_fbeta, fbeta)) != hipSuccess) return bad(e, "upload fbeta");
+        std::vector<double> lb(pbg::kLbSize, 0.0);
+        for (int m = 1; m <= 16; ++m) lb[m] = lb[m - 1] + fk[m - 1];
+        for (int d = 3; d <= 16; ++d) {
+            double run = 1e300;   // suffix minimum over q' >= q
+            for (int q = 63; q >= 4; --q) {
+                for (int cc = 0; cc <= d - 2; ++cc) run = std::min(run, beta[q << 16 | d << 8 | cc]);
+                lb[17 + (q - 4) * 17 + d] = run;
+            }
+        }
+        if ((e = upload(&c->d_lb, lb)) != hipSuccess) return bad(e, "upload lb");
     }
     // Tajima constants are indexed by population size and built for n = sm->n (pop_sfs.cpp:53-56)
     std::vector<double> a1, a2, e1, e2;
@@ -220,6 +231,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     c->dt.beta = c->d_beta;
     c->dt.lhet = c->d_lhet;
     c->dt.fbeta = c->d_fbeta;
+    c->dt.lb = c->d_lb;
     c->dt.a1 = c->d_sfs;
     c->dt.a2 = c->d_sfs + L;
     c->dt.e1 = c->d_sfs + 2 * L;
@@ -239,7 +251,7 @@ void pbg_destroy(pbg_ctx *c) {
         (void)hipEventDestroy(c->ev_deep);
     }
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
-                    (void *)c->d_fbeta, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff,
+                    (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
                     (void *)c->deep.blk_cnt, (void *)c->deep.raw,
                     (void *)c->d_segcnt, (void *)c->d_synth})

@@ -39,11 +39,17 @@ struct DevTables {
     // fbeta_index(q, n, c, w).  The product is the one IEEE double multiply errmod_cal does
     // per key (pop_utils.cpp:311), so the table value is bit-identical to it.
     const double *fbeta;  // [64*17*16*16]
+    // one-error bound (call_slow_kernel): [0, 17) fk_prefix[m] = sum_{w < m} fk[w]; then
+    // [17 + (q - 4) * 17 + d] = min over q' in [q, 63], c in [0, d - 2] of beta[q'<<16|d<<8|c]
+    // (q 4..63, d 3..16): with m0 / m1 reference-base keys per strand, all of quality >= q,
+    // errmod_cal's bsum of that base is >= (fk_prefix[m0] + fk_prefix[m1]) * bmin[q][d]
+    const double *lb;     // [17 + 60 * 17]
     const double *a1, *a2, *e1, *e2;          // Tajima/Fay-Wu constants (pop_sfs.cpp:511-571)
     const double *r2;     // concatenated per-population r^2 tables, see r2_off
     int32_t r2_off[PBG_MAX_POPS];             // offset of population p's (n_p+1)^3 table
 };
 
+constexpr int kLbSize = 17 + 60 * 17;
 constexpr int kFbetaN = 17;   // n in [0, 16]
 __host__ __device__ inline uint32_t fbeta_index(uint32_t q, uint32_t n, uint32_t c, uint32_t w) {
     return ((q * kFbetaN + n) << 8) | (c << 4) | w;

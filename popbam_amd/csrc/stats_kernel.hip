@@ -179,7 +179,10 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     // seg rows of word c (in window): bit mask + types; `store` gets (index, types)
     // the window's 16-byte words in groups of kLoadAhead per lane: a group's loads are issued
     // together, so the dependent compaction steps wait on one memory latency per group
-    constexpr int kLoadAhead = 4;
+#ifndef PBG_WIN_AHEAD
+#define PBG_WIN_AHEAD 4
+#endif
+    constexpr int kLoadAhead = PBG_WIN_AHEAD;
     auto compact = [&](M *dst, uint32_t cap, bool count_sites, int &my_counted) -> uint32_t {
         uint32_t S = 0;
         uint4 qa[kLoadAhead];
@@ -268,6 +271,16 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         if (A.seg_count) A.seg_count[w] = (int)S;
     }
     const int npairs = np * (np - 1);
+#ifdef PBG_WIN_TIME_LOADS   // timing experiments only: the row pass alone
+    if (S < 1000000u) {   // no ZnS chains to run (window_zns_kernel reads var_count / zoff)
+        if ((stats & PBG_S_ZNS) && lane < np) {
+            A.var_count[(size_t)w * np + lane] = 0;
+            A.zoff[(size_t)w * np + lane] = 0;
+            A.ld_ns[(size_t)w * np + lane] = 0;
+        }
+        return;
+    }
+#endif
 
     // ---- bitplanes (hap.seq) and the u16 pairwise-difference matrix
     uint64_t *plane = nullptr;
@@ -826,7 +839,10 @@ __device__ __forceinline__ void add_row(double &acc, double r) {
         add_row<J + 1>(acc, r);
     }
 }
-constexpr int kZnsRowUnroll = 2;
+#ifndef PBG_ZNS_UNROLL
+#define PBG_ZNS_UNROLL 2
+#endif
+constexpr int kZnsRowUnroll = PBG_ZNS_UNROLL;
 template <class M>
 __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A,
                                                              int r2_lds) {
@@ -861,12 +877,34 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
     __syncthreads();
     auto run = [&](const M *lst, const double *r2p) -> double {
         const int vm1 = V > 0 ? V - 1 : 0;
+#ifndef PBG_ZNS_ROWSTEP
+        // Lane g holds pair 16s + g of the chain's flat pair sequence (rows a ascending, b
+        // ascending within a row): a step spans row ends, so only the chain's last step adds
+        // padding.  Pair (a, b) past its row's end (b >= V) moves to (a + 1, a + 2 + (b - V)).
+        int a = 0, b = 1 + g;
+        auto norm = [&]() {
+            while ((b >= V) & (a < V - 1)) {
+                b += a + 2 - V;
+                ++a;
+            }
+        };
+        norm();
+#else
         int a = 0, b0 = 1;
+#endif
         double acc = 0.0;
         while (__ballot(a < V - 1)) {   // wave-uniform: until the wave's four chains are done
             double r[kZnsRowUnroll];
 #pragma unroll
             for (int u = 0; u < kZnsRowUnroll; ++u) {
+#ifndef PBG_ZNS_ROWSTEP
+                const bool ok = (a < V - 1) & (b < V);
+                const M ta = lst[min(a, vm1)], tb = lst[min(b, vm1)];
+                const double rv = r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
+                r[u] = ok ? rv : 0.0;
+                b += 16;
+                norm();
+#else
                 const int b = b0 + g;
                 const bool ok = (a < V - 1) & (b < V);
                 const M ta = lst[min(a, vm1)], tb = lst[min(b, vm1)];
@@ -876,6 +914,7 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
                 const bool nxt = (b0 >= V) & (a < V - 1);
                 a += nxt ? 1 : 0;
                 b0 = nxt ? a + 1 : b0;
+#endif
             }
 #ifdef PBG_ZNS_DPP
 #pragma unroll
@@ -889,6 +928,11 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const double2 *sv2 = reinterpret_cast<const double2 *>(sv);
+#ifndef PBG_ZNS_ALL_LANES
+            // only the row's first lane keeps the sum (it writes the output): one active lane
+            // per row, so each broadcast read moves 4 lanes' words instead of the wave's 64
+            if (g == 0)
+#endif
 #pragma unroll
             for (int x = 0; x < 8 * kZnsRowUnroll; ++x) {
                 const double2 v = sv2[x];

@@ -150,6 +150,7 @@ class HotPath:
                  device: str = "cuda"):
         self.ctx, self.synth, self.stats = ctx, synth, stats
         self.rows = torch.zeros(synth.n_sites * ctx.row_bytes, dtype=torch.uint8, device=device)
+        self.windows = [tuple(ab) for ab in windows]
         w = torch.tensor([x for ab in windows for x in ab], dtype=torch.int32)
         self.wins = w.to(device)
         self.n_win = len(windows)
@@ -194,3 +195,84 @@ class HotPath:
     def step(self, stream=None):
         self.call(stream)
         self.window_stats(stream)
+
+    # ---- pipelined step: the contig in pieces, statistics of piece i beside the call of i+1
+    def split_points(self, pieces: int) -> list[int]:
+        """Row positions [0, p1, ..., n_sites) splitting the batch into about `pieces` equal
+        parts, each split a multiple of the 64-position block with no window across it (so
+        every window's rows come from one piece's call)."""
+        import bisect
+        n = self.synth.n_sites
+        wins = sorted(self.windows)
+        begs = [b for b, _ in wins]
+        reach, m = [], 0   # reach[i] = max end of wins[:i+1]
+        for _, e in wins:
+            m = max(m, e)
+            reach.append(m)
+
+        def free(p):   # no window with beg < p < end
+            i = bisect.bisect_left(begs, p)   # wins[:i] begin before p
+            return i == 0 or reach[i - 1] <= p
+
+        pts = [0]
+        for j in range(1, pieces):
+            p = (n * j // pieces) // SITE_BLOCK * SITE_BLOCK
+            while p > pts[-1] and not free(p):
+                p -= SITE_BLOCK
+            if p > pts[-1]:
+                pts.append(p)
+        pts.append(n)
+        return pts
+
+    def pipeline(self, pieces: int, device: str = "cuda"):
+        """Per-piece sub-batches (views into the synthetic batch: block_off keeps absolute key
+        offsets, so keys[] is shared), row slices, window lists and output slices."""
+        n = self.ctx.params.n_samples
+        rb, kb = self.ctx.row_bytes, self.ctx.k_bytes
+        pts = self.split_points(pieces)
+        s = self.synth
+        per_win = {k: (t.numel() // max(1, self.n_win), t.element_size()) for k, t in self.out.t.items()}
+        fields = self.fields_for(self.stats)
+        self.pieces = []
+        for p0, p1 in zip(pts[:-1], pts[1:]):
+            pl = _lib.PbgPileup(p1 - p0, s.pos0 + p0, _ptr(s.ref) + p0, _ptr(s.k) + p0 * n * kb,
+                                _ptr(s.rmsq) + p0 * n * 4, _ptr(s.block_off) + (p0 // SITE_BLOCK) * 8, _ptr(s.keys))
+            idx = [i for i, (b, e) in enumerate(self.windows) if b >= p0 and e <= p1]
+            assert idx == list(range(idx[0], idx[-1] + 1)) if idx else True
+            w = torch.tensor([x for i in idx for x in (self.windows[i][0] - p0, self.windows[i][1] - p0)],
+                             dtype=torch.int32).to(device)
+            o = _lib.PbgWindowOut()
+            w0 = idx[0] if idx else 0
+            for k in fields:
+                per, es = per_win[k]
+                setattr(o, k, _ptr(self.out.t[k]) + w0 * per * es)
+            self.pieces.append((pl, _ptr(self.rows) + p0 * rb, p1 - p0, w, len(idx), o))
+        assert sum(pc[4] for pc in self.pieces) == self.n_win, "a window spans a piece border"
+        self.ev_done = [torch.cuda.Event() for _ in self.pieces]
+        return pts
+
+    def call_pieces(self, stream):
+        for pl, rows, _, _, _, _ in self.pieces:
+            self.ctx.check(self.ctx.lib.pbg_call_sites(self.ctx.h, C.byref(pl), rows, None, stream.cuda_stream),
+                           "pbg_call_sites")
+
+    def stats_pieces(self, stream):
+        for _, rows, nrows, w, nw, o in self.pieces:
+            if nw:
+                self.ctx.check(self.ctx.lib.pbg_window_stats(self.ctx.h, rows, nrows, _ptr(w), nw, C.byref(self.opts),
+                                                             C.byref(o), stream.cuda_stream), "pbg_window_stats")
+
+    def step_pipelined(self, call_stream, stats_stream):
+        """call(piece i) on call_stream; stats(piece i) on stats_stream after it, so the
+        statistics of piece i run beside the call of piece i+1.  Same work as step()."""
+        lib, h = self.ctx.lib, self.ctx.h
+        stats_stream.wait_stream(call_stream)   # previous step's users of rows / outputs
+        call_stream.wait_stream(stats_stream)
+        for (pl, rows, nrows, w, nw, o), ev in zip(self.pieces, self.ev_done):
+            self.ctx.check(lib.pbg_call_sites(h, C.byref(pl), rows, None, call_stream.cuda_stream), "pbg_call_sites")
+            ev.record(call_stream)
+            stats_stream.wait_event(ev)
+            if nw:
+                self.ctx.check(lib.pbg_window_stats(h, rows, nrows, _ptr(w), nw, C.byref(self.opts), C.byref(o),
+                                                    stats_stream.cuda_stream), "pbg_window_stats")
+        call_stream.wait_stream(stats_stream)

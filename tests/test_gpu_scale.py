@@ -355,3 +355,33 @@ def test_inconsistent_batch_is_reported(gpu_lib):
         assert ctx.lib.pbg_check(ctx.h, None) == _lib.PBG_E_BATCH
         assert ctx.lib.pbg_check(ctx.h, None) == _lib.PBG_OK
     ctx.close()
+
+
+@pytest.mark.parametrize("n,npops,pieces", [(12, 2, 4), (24, 3, 3), (96, 3, 5)])
+def test_pipelined_pieces_equal_one_step(gpu_lib, n, npops, pieces):
+    """bench.py's pipelined step (the contig's call in pieces at window borders, each piece's
+    statistics on a second stream beside the next piece's call) writes the same rows and the
+    same window outputs, byte for byte, as one call + one statistics launch."""
+    import torch
+    from popbam_amd import _lib, workload
+    stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS
+    ctx, params = _ctx(n, npops)
+    n_sites = 2_000_000 + 37
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + n)
+    wins = workload.reference_windows(0, n_sites, 10_000)
+    one = workload.HotPath(ctx, syn, wins, stats)
+    one.step()
+    ctx.sync_check()
+    two = workload.HotPath(ctx, syn, wins, stats)
+    pts = two.pipeline(pieces)
+    assert len(pts) == pieces + 1 and all(p % 64 == 0 for p in pts[:-1])
+    s1, s2 = torch.cuda.current_stream(), torch.cuda.Stream()
+    for _ in range(2):
+        two.step_pipelined(s1, s2)
+    torch.cuda.synchronize()
+    ctx.sync_check()
+    assert torch.equal(one.rows, two.rows)
+    for k in workload.HotPath.fields_for(stats):
+        assert torch.equal(one.out.t[k].view(torch.uint8), two.out.t[k].view(torch.uint8)), k
+    assert int(one.out.t["segsites"].sum()) > 0
+    ctx.close()

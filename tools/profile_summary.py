@@ -49,7 +49,8 @@ def main():
            "fetch_size_kib": fetch[k], "write_size_kib": write[k], "fetch_correction": 2.0,
            "hbm_bytes_per_launch": int(fetch[k] * 1024 * 2 + write[k] * 1024),
            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on bench.py --steps 2, {tag}",
-           "algorithmic_bytes_per_launch": b["roofline"]["bytes_per_launch"], "layout": "keys16"}
+           "algorithmic_bytes_per_launch": b["roofline"]["bytes_per_launch"], "layout": "keys16",
+           "pieces": cfg.get("pieces", 1)}
     json.dump(pmc, open(os.path.join(top, f"pmc_{k}.json"), "w"), indent=1)
     print(json.dumps(pmc, indent=1))
 
