@@ -171,7 +171,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
                 }
                 d.sample_pop[v] = (int8_t)i;
             }
-    for (int k = 0; k <= 16; ++k) d.rms_thr[k] = rms_threshold(k, p->min_rmsQ, p->min_depth, p->max_depth);
+    for (int k = 0; k <= PBG_FAST_MAX; ++k) d.rms_thr[k] = rms_threshold(k, p->min_rmsQ, p->min_depth, p->max_depth);
     d.sfs_stride = 1;
     for (int i = 0; i < p->n_pops; ++i) d.sfs_stride = std::max(d.sfs_stride, p->pop_n[i] + 1);
     auto bad = [&](hipError_t e, const char *what) {
@@ -183,6 +183,14 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     if (e != hipSuccess) return bad(e, "hipSetDevice");
     std::vector<double> fk, beta, lhet;
     pbg::build_errmod_tables(fk, beta, lhet);
+    // the scan's reference-only shortcut needs every beta[q][n][c < n] > 0 (q >= 4, n <= PBG_FAST_MAX)
+    for (int q = 4; q < 64; ++q)
+        for (int nn = 1; nn <= PBG_FAST_MAX; ++nn)
+            for (int cc = 0; cc < nn; ++cc)
+                if (!(beta[q << 16 | nn << 8 | cc] > 0.0)) {
+                    pbg_destroy(c);
+                    return fail(nullptr, PBG_E_ARG, "errmod beta table has a non-positive entry");
+                }
     if ((e = upload(&c->d_fk, fk)) != hipSuccess) return bad(e, "upload fk");
     if ((e = upload(&c->d_beta, beta)) != hipSuccess) return bad(e, "upload beta");
     if ((e = upload(&c->d_lhet, lhet)) != hipSuccess) return bad(e, "upload lhet");

@@ -12,6 +12,11 @@ namespace pbg {
 constexpr int kBlockThreads = 256;     // 4 wave64 per workgroup
 constexpr int kSiteBlock = PBG_SITE_BLOCK;
 
+// reference-only tasks (every key on the reference base) are settled by the scan kernel up to
+// this many keys (16 or 32)
+#ifndef PBG_FAST_MAX
+#define PBG_FAST_MAX 32
+#endif
 // Parameters passed by value to the kernels (kernarg segment).
 struct DevParams {
     int32_t n, npops;
@@ -27,7 +32,7 @@ struct DevParams {
     // sum mapQ^2 >= rms_thr[d].  rms = (unsigned)(sqrtf((float)rmsq / d) + 0.499) is monotone in
     // rmsq, so "rms >= min_rmsQ && min_depth <= d <= max_depth" is one threshold per d, found on
     // the host with the same IEEE float division and square root (rms_threshold, api.cpp).
-    uint32_t rms_thr[17];
+    uint32_t rms_thr[PBG_FAST_MAX + 1];
 };
 
 // Host-built tables resident in HBM for the lifetime of a context.
