@@ -75,9 +75,22 @@ struct SynthSite {
     int ref_idx, alt, snp;
     uint32_t f16;
 };
+// the site's fields from its hash (kernels hash each position once and share it across samples)
+__host__ __device__ inline SynthSite synth_site_h(uint64_t h) {
+    SynthSite s;
+    s.h = h;
+    s.ref_idx = (int)(s.h & 3);
+    s.snp = ((s.h >> 2) & 0x3FF) < 12;          // theta ~ 0.012
+    s.alt = (s.ref_idx + 1 + (int)((((s.h >> 12) & 0xFFFFu) * 3u) >> 16)) & 3;   // 1..3 steps away
+    s.f16 = (uint32_t)((s.h >> 16) & 0xFFFF);   // derived allele frequency
+    return s;
+}
+__host__ __device__ inline uint64_t synth_site_hash(uint64_t seed, int contig, uint64_t pos) {
+    return splitmix64(seed ^ splitmix64(pos ^ ((uint64_t)(uint32_t)contig << 40)));
+}
 __host__ __device__ inline SynthSite synth_site(uint64_t seed, int contig, uint64_t pos) {
     SynthSite s;
-    s.h = splitmix64(seed ^ splitmix64(pos ^ ((uint64_t)(uint32_t)contig << 40)));
+    s.h = synth_site_hash(seed, contig, pos);
     s.ref_idx = (int)(s.h & 3);
     s.snp = ((s.h >> 2) & 0x3FF) < 12;          // theta ~ 0.012
     s.alt = (s.ref_idx + 1 + (int)((((s.h >> 12) & 0xFFFFu) * 3u) >> 16)) & 3;   // 1..3 steps away

@@ -130,6 +130,7 @@ class GenomePass:
         self.call_stream = torch.cuda.Stream(device=device)
         self.ready = [torch.cuda.Event() for _ in range(2)]
         self.free = [torch.cuda.Event() for _ in range(2)]
+        self.slot_used = [False, False]   # a call on the slot's buffer has been enqueued (free[] recorded)
         # windows of every segment as row indices into the genome-resident rows; one statistics
         # launch per group of segments whose rows stay below 2^31 (pbg_window is int32)
         self.win_lists = []
@@ -188,8 +189,10 @@ class GenomePass:
         for c in range(len(self.chunks)):
             slot = c & 1
             with torch.cuda.stream(self.gen_stream):
-                if c >= 2:
+                # the slot's previous call (this pass or the previous one) must be done with it
+                if self.slot_used[slot]:
                     self.gen_stream.wait_event(self.free[slot])
+                self.slot_used[slot] = True
                 self._generate(c, slot)
                 self.ready[slot].record(self.gen_stream)
             with torch.cuda.stream(self.call_stream):
