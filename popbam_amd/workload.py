@@ -248,7 +248,8 @@ class HotPath:
                 setattr(o, k, _ptr(self.out.t[k]) + w0 * per * es)
             self.pieces.append((pl, _ptr(self.rows) + p0 * rb, p1 - p0, w, len(idx), o))
         assert sum(pc[4] for pc in self.pieces) == self.n_win, "a window spans a piece border"
-        self.ev_done = [torch.cuda.Event() for _ in self.pieces]
+        self.ev_done = [torch.cuda.Event() for _ in self.pieces]    # piece's call enqueued
+        self.ev_stats = [torch.cuda.Event() for _ in self.pieces]   # piece's statistics enqueued
         return pts
 
     def call_pieces(self, stream):
@@ -263,11 +264,21 @@ class HotPath:
                                                              C.byref(o), stream.cuda_stream), "pbg_window_stats")
 
     def step_pipelined(self, call_stream, stats_stream):
-        """call(piece i) on call_stream; stats(piece i) on stats_stream after it, so the
-        statistics of piece i run beside the call of piece i+1.  Same work as step()."""
+        """call(piece i) on call_stream; stats(piece i) on stats_stream after it.  The statistics
+        of piece i run beside the call of piece i+1, and the last piece's beside the next step's
+        first call; a piece's call waits only for the previous statistics of that same piece
+        (the one reader of its rows).  Same work as step(); the caller synchronises both
+        streams before reading outputs."""
         lib, h = self.ctx.lib, self.ctx.h
-        stats_stream.wait_stream(call_stream)   # previous step's users of rows / outputs
-        call_stream.wait_stream(stats_stream)
+        for (pl, rows, nrows, w, nw, o), ev, done in zip(self.pieces, self.ev_done, self.ev_stats):
+            call_stream.wait_event(done)   # no-op until the piece's statistics have been enqueued once
+            self.ctx.check(lib.pbg_call_sites(h, C.byref(pl), rows, None, call_stream.cuda_stream), "pbg_call_sites")
+            ev.record(call_stream)
+            stats_stream.wait_event(ev)
+            if nw:
+                self.ctx.check(lib.pbg_window_stats(h, rows, nrows, _ptr(w), nw, C.byref(self.opts), C.byref(o),
+                                                    stats_stream.cuda_stream), "pbg_window_stats")
+            done.record(stats_stream)
         for (pl, rows, nrows, w, nw, o), ev in zip(self.pieces, self.ev_done):
             self.ctx.check(lib.pbg_call_sites(h, C.byref(pl), rows, None, call_stream.cuda_stream), "pbg_call_sites")
             ev.record(call_stream)

@@ -359,9 +359,9 @@ def test_inconsistent_batch_is_reported(gpu_lib):
 
 @pytest.mark.parametrize("n,npops,pieces", [(12, 2, 4), (24, 3, 3), (96, 3, 5)])
 def test_pipelined_pieces_equal_one_step(gpu_lib, n, npops, pieces):
-    """bench.py's pipelined step (the contig's call in pieces at window borders, each piece's
-    statistics on a second stream beside the next piece's call) writes the same rows and the
-    same window outputs, byte for byte, as one call + one statistics launch."""
+    """bench.py's pipelined steps (the contig's call in pieces at window borders, each piece's
+    statistics on a second stream beside the next piece's call, across steps too) write the
+    same rows and the same window outputs, byte for byte, as one call + one statistics launch."""
     import torch
     from popbam_amd import _lib, workload
     stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS
@@ -376,7 +376,7 @@ def test_pipelined_pieces_equal_one_step(gpu_lib, n, npops, pieces):
     pts = two.pipeline(pieces)
     assert len(pts) == pieces + 1 and all(p % 64 == 0 for p in pts[:-1])
     s1, s2 = torch.cuda.current_stream(), torch.cuda.Stream()
-    for _ in range(2):
+    for _ in range(3):   # back-to-back steps: the last piece's statistics overlap the next first call
         two.step_pipelined(s1, s2)
     torch.cuda.synchronize()
     ctx.sync_check()

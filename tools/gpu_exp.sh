@@ -1,10 +1,9 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R"; mkdir -p gpurun_out/ab3
-for v in head main head main; do
-  if [ $v = main ]; then L=""; else L=$R/popbam_amd/variants/$v/libpopbam_gpu.so; fi
-  POPBAM_GPU_LIB=$L timeout -k 10 200 python3 bench.py --config 3 --steps 2 --warmup 1 --cpu-sample 0 > gpurun_out/ab3/$v.json 2> gpurun_out/ab3/$v.err || { echo "$v failed"; tail -2 gpurun_out/ab3/$v.err; exit 1; }
-  python3 -c "import json; d=json.load(open('gpurun_out/ab3/$v.json')); print('$v', d['value'], d['ms_per_step'], d['roofline']['ms_per_launch'], d['roofline']['frac'], d['call_stage'])"
+cd "$R"; mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_scale.py -k "pipelined" > gpurun_out/pytest_pipe.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_pipe.log; exit 1; }
+tail -1 gpurun_out/pytest_pipe.log
+for p in 1 2 3 4 1 2 3; do
+  timeout -k 10 120 python bench.py --steps 20 --warmup 3 --cpu-sample 0 --pieces $p > gpurun_out/bench_p$p.json 2>gpurun_out/bench_p$p.err || { tail -3 gpurun_out/bench_p$p.err; exit 1; }
+  python3 -c "import json; d=json.load(open('gpurun_out/bench_p$p.json')); print('pieces $p', d['value'], d['ms_per_step'], d['roofline']['ms_per_launch'], d['call_stage']['ms_library_events'], d['window_stats']['ms_serial'])"
 done
-timeout -k 10 300 python3 bench.py --config 4 --steps 2 --warmup 1 --cpu-sample 0 > gpurun_out/ab3/c4.json 2> gpurun_out/ab3/c4.err || { echo "c4 failed"; tail -2 gpurun_out/ab3/c4.err; exit 1; }
-python3 -c "import json; d=json.load(open('gpurun_out/ab3/c4.json')); print('c4', d['value'], d['ms_per_step'], d['roofline']['ms_per_launch'], d['call_stage'])"
