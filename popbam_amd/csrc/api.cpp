@@ -172,6 +172,8 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
                 d.sample_pop[v] = (int8_t)i;
             }
     for (int k = 0; k <= PBG_FAST_MAX; ++k) d.rms_thr[k] = rms_threshold(k, p->min_rmsQ, p->min_depth, p->max_depth);
+    d.rmsq_thr[0] = p->min_rmsQ <= 0 ? 0u : 0xFFFFFFFFu;
+    for (int k = 1; k <= 16; ++k) d.rmsq_thr[k] = rms_threshold(k, p->min_rmsQ, 1, 1 << 30);
     d.sfs_stride = 1;
     for (int i = 0; i < p->n_pops; ++i) d.sfs_stride = std::max(d.sfs_stride, p->pop_n[i] + 1);
     auto bad = [&](hipError_t e, const char *what) {

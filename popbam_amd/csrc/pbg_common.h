@@ -33,6 +33,9 @@ struct DevParams {
     // rmsq, so "rms >= min_rmsQ && min_depth <= d <= max_depth" is one threshold per d, found on
     // the host with the same IEEE float division and square root (rms_threshold, api.cpp).
     uint32_t rms_thr[PBG_FAST_MAX + 1];
+    // qfilter's rms test alone, for k = 0..16 keys: rms >= min_rmsQ iff sum mapQ^2 >= rmsq_thr[k]
+    // (k = 0: rms is 0 -- the x86 NaN conversion -- so 0 when min_rmsQ <= 0, else never)
+    uint32_t rmsq_thr[17];
 };
 
 // Host-built tables resident in HBM for the lifetime of a context.

@@ -933,11 +933,20 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
             // per row, so each broadcast read moves 4 lanes' words instead of the wave's 64
             if (g == 0)
 #endif
+            {
+                // every read issued before the first add (sched_barrier): the adds then run back
+                // to back instead of each pair waiting on its own LDS round trip
+                double2 v[8 * kZnsRowUnroll];
 #pragma unroll
-            for (int x = 0; x < 8 * kZnsRowUnroll; ++x) {
-                const double2 v = sv2[x];
-                acc += v.x;
-                acc += v.y;
+                for (int x = 0; x < 8 * kZnsRowUnroll; ++x) v[x] = sv2[x];
+#ifndef PBG_ZNS_NO_AHEAD
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+                for (int x = 0; x < 8 * kZnsRowUnroll; ++x) {
+                    acc += v[x].x;
+                    acc += v[x].y;
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
