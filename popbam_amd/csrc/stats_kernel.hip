@@ -840,7 +840,7 @@ __device__ __forceinline__ void add_row(double &acc, double r) {
     }
 }
 #ifndef PBG_ZNS_UNROLL
-#define PBG_ZNS_UNROLL 2
+#define PBG_ZNS_UNROLL 1   // steps per pipelined round (1: 0.37 ms of statistics at configs[2]; 2: 0.38; 4: 0.40)
 #endif
 constexpr int kZnsRowUnroll = PBG_ZNS_UNROLL;
 template <class M>
@@ -849,7 +849,7 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
     constexpr int kStage = zns_stage<M>(), kStride = zns_stride<M>();
     extern __shared__ __align__(16) double s_dyn[];
     // a step's r^2 per chain; +2 doubles per chain so the four rows of a wave read different banks
-    __shared__ __align__(16) double s_val[16][16 * kZnsRowUnroll + 2];
+    __shared__ __align__(16) double s_val[16][2 * (16 * kZnsRowUnroll + 2)];   // two halves (pipelined rounds)
     double *s_r2t = s_dyn;                                                      // [r2_lds]
     M *s_t = reinterpret_cast<M *>(s_dyn + r2_lds);                            // [16][kStride] masks
     for (int i = threadIdx.x; i < r2_lds; i += 256) s_r2t[i] = T.r2[i];
@@ -954,9 +954,72 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
         }
         return acc;
     };
+#ifndef PBG_ZNS_NO_PIPE
+    // Software-pipelined rounds: round i's values are read from one half of the chain's LDS
+    // buffer while round i+1's r^2 values are produced into registers (their list / table loads
+    // in flight during the reads, their VALU free to interleave with round i's dependent adds --
+    // one basic block, no exec-mask branches), then stored to the other half.  Row-step order
+    // (b0 .. b0+15 of row a per step; lanes past the row's end give +0.0).
+    auto run_pipe = [&](const M *lst, const double *r2p) -> double {
+        constexpr int U = kZnsRowUnroll, kHalf = 16 * U + 2;
+        const int vm1 = V > 0 ? V - 1 : 0;
+        int a = 0, b0 = 1;
+        double r[U];
+        auto produce = [&]() {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int b = b0 + g;
+                const bool ok = (a < V - 1) & (b < V);
+                const M ta = lst[min(a, vm1)], tb = lst[min(b, vm1)];
+                const double rv = r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
+                r[u] = ok ? rv : 0.0;
+                b0 += 16;
+                const bool nxt = (b0 >= V) & (a < V - 1);
+                a += nxt ? 1 : 0;
+                b0 = nxt ? a + 1 : b0;
+            }
+        };
+        auto put = [&](int c) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) sv[c * kHalf + 16 * u + g] = r[u];
+        };
+        auto sync = [&]() {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        double acc = 0.0;
+        bool live = __ballot(a < V - 1) != 0;   // wave-uniform: round 0 has pairs
+        produce();
+        put(0);
+        sync();
+        int c = 0;
+        while (live) {
+            const double2 *sv2 = reinterpret_cast<const double2 *>(sv + c * kHalf);
+            double2 v[8 * U];
+#pragma unroll
+            for (int x = 0; x < 8 * U; ++x) v[x] = sv2[x];
+            live = __ballot(a < V - 1) != 0;   // the next round has pairs
+            produce();
+#pragma unroll
+            for (int x = 0; x < 8 * U; ++x) {   // pair order: step u, lane 0..15
+                acc += v[x].x;
+                acc += v[x].y;
+            }
+            put(c ^ 1);
+            sync();
+            c ^= 1;
+        }
+        return acc;
+    };
+    double acc;
+    if (staged) acc = r2_lds ? run_pipe(lt, s_r2t + r2o) : run_pipe(lt, T.r2 + r2o);
+    else acc = r2_lds ? run_pipe(L, s_r2t + r2o) : run_pipe(L, T.r2 + r2o);
+#else
     double acc;
     if (staged) acc = r2_lds ? run(lt, s_r2t + r2o) : run(lt, T.r2 + r2o);
     else acc = r2_lds ? run(L, s_r2t + r2o) : run(L, T.r2 + r2o);
+#endif
     if (g == 0 && ch < nch) {
         const uint32_t w = ch / (uint32_t)np;
         double val = 0.0;

@@ -1,7 +1,6 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
-timeout -k 10 60 ./tools/ubench/fadd_chain || exit 1
-BENCH_ARGS="--steps 10 --warmup 2 --cpu-sample 0" bash tools/ab.sh head slim znoahead zahead zahead_u4 head slim zahead || exit 1
-timeout -k 10 700 python -u -m pytest -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests > gpurun_out/pytest_all.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_all.log; exit 1; }
-tail -2 gpurun_out/pytest_all.log
+BENCH_ARGS="--steps 10 --warmup 2 --cpu-sample 0" bash tools/ab.sh nopipe pipe pipe_u4 pipe_u1 nopipe pipe || exit 1
+timeout -k 10 700 python -u -m pytest -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_scale.py tests/test_gpu_golden.py tests/test_wide_samples.py tests/test_genome.py > gpurun_out/pytest_stats.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_stats.log; exit 1; }
+tail -2 gpurun_out/pytest_stats.log
