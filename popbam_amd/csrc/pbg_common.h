@@ -199,6 +199,10 @@ struct DeepBufs {
 #define PBG_QGROUP 16
 #endif
 constexpr int kQueueGroup = PBG_QGROUP;   // blocks per wave in the queue kernels
+#ifndef PBG_DEEP_GROUP
+#define PBG_DEEP_GROUP 64
+#endif
+constexpr int kDeepGroup = PBG_DEEP_GROUP;   // blocks per wave in call_deepq_kernel (few deep tasks)
 
 // A device pileup batch as the kernels see it (pbg_pileup with the k width resolved).
 struct Batch {

@@ -1,8 +1,6 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests > gpurun_out/pytest_all.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_all.log; exit 1; }
-tail -2 gpurun_out/pytest_all.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1
-timeout -k 10 200 python3 bench.py > gpurun_out/bench.log 2>&1 || exit 1
-python3 -c "import json; d=json.loads(open('gpurun_out/bench.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['call_stage']['ms_library_events'], d['window_stats']['ms_serial'])"
+BENCH_ARGS="--steps 10 --warmup 2 --cpu-sample 0" bash tools/ab.sh head dg64 dg32 head dg64 dg32 || exit 1
+timeout -k 10 400 python -u -m pytest -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_scale.py tests/test_gpu_golden.py -k "call or rows_only or fixture or deep or golden" > gpurun_out/pytest_call.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_call.log; exit 1; }
+tail -2 gpurun_out/pytest_call.log
