@@ -151,7 +151,16 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
 
     const int n = P.n, np = P.npops;
     const int lane = threadIdx.x;
+#ifdef PBG_WIN_SKIP   // timing experiments only: statistics left out of this kernel
+    const uint32_t stats = A.stats & ~(uint32_t)(PBG_WIN_SKIP);
+    if ((A.stats & PBG_S_ZNS) && ((PBG_WIN_SKIP) & PBG_S_ZNS) && lane < np) {   // window_zns_kernel runs no chain
+        A.var_count[(size_t)w * np + lane] = 0;
+        A.zoff[(size_t)w * np + lane] = 0;
+        A.ld_ns[(size_t)w * np + lane] = 0;
+    }
+#else
     const uint32_t stats = A.stats;
+#endif
     const int64_t wb = A.wins[w].beg, we = A.wins[w].end > A.wins[w].beg ? A.wins[w].end : A.wins[w].beg;
     const bool ld_ws = (stats & (PBG_S_OMEGA | PBG_S_WALL)) != 0;  // window_ld_kernel reads the seg list
     for (int i = lane; i < L.r2lds; i += 64) s_r2[i] = T.r2[i];

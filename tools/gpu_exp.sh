@@ -1,7 +1,14 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R"; mkdir -p gpurun_out/ab3
-timeout -k 10 200 python3 bench.py --config 3 --steps 2 --warmup 1 --cpu-sample 0 > gpurun_out/ab3/c3.json 2> gpurun_out/ab3/c3.err || { tail -3 gpurun_out/ab3/c3.err; exit 1; }
-python3 -c "import json; d=json.load(open('gpurun_out/ab3/c3.json')); print('c3', d['value'], d['ms_per_step'], d['roofline'])"
-timeout -k 10 300 python3 bench.py --config 4 --steps 2 --warmup 1 --cpu-sample 0 > gpurun_out/ab3/c4.json 2> gpurun_out/ab3/c4.err || { tail -3 gpurun_out/ab3/c4.err; exit 1; }
-python3 -c "import json; d=json.load(open('gpurun_out/ab3/c4.json')); print('c4', d['value'], d['ms_per_step'], d['roofline'])"
+cd "$R"; mkdir -p gpurun_out
+export TMPDIR=/tmp
+for v in base skipz skipzs skipzsn; do
+  rm -rf gpurun_out/prof_v
+  POPBAM_GPU_LIB=$R/popbam_amd/variants/$v/libpopbam_gpu.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$R/gpurun_out/prof_v" -o run \
+    -- python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/prof_v.log 2>&1 || exit 1
+  python3 -c "
+import csv
+for r in csv.DictReader(open('gpurun_out/prof_v/run_kernel_stats.csv')):
+    if r['Name'].startswith('window'): print('$v', r['Name'][:28], round(float(r['AverageNs'])/1e3, 1), 'us')
+"
+done
