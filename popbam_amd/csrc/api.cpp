@@ -36,9 +36,11 @@ struct pbg_ctx {
     struct Plan {
         const void *wins;
         uint32_t n_win, n_rows, stats;
+        uint64_t zstride;   // ZnS list words per window at fixed places (0: pool)
     };
     std::vector<Plan> plans;
-    uint64_t *d_ws = nullptr, *d_wsoff = nullptr;
+    uint64_t *d_ws = nullptr, *d_wsoff = nullptr, *d_zns = nullptr;
+    size_t zns_cap = 0;   // bytes of d_zns
     size_t ws_cap = 0, wsoff_cap = 0, segcnt_cap = 0;
     int32_t *d_segcnt = nullptr;
     // samples deeper than the register sort width (call kernel): queues + parked info bytes
@@ -261,7 +263,7 @@ void pbg_destroy(pbg_ctx *c) {
         (void)hipEventDestroy(c->ev_deep);
     }
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
-                    (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff,
+                    (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, (void *)c->d_zns,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
                     (void *)c->deep.blk_cnt, (void *)c->deep.raw,
                     (void *)c->d_segcnt, (void *)c->d_synth})
@@ -432,18 +434,23 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     const int n = c->dp.n, np = c->dp.npops;
     const uint64_t mw = c->row_bytes == 16 ? 2 : 1;
     bool known = false;
+    uint64_t zstride = 0;
     for (const auto &pl : c->plans)
-        known |= pl.wins == (const void *)wins && pl.n_win == n_win && pl.n_rows == n_rows && pl.stats == o->stats;
+        if (pl.wins == (const void *)wins && pl.n_win == n_win && pl.n_rows == n_rows && pl.stats == o->stats) {
+            known = true;
+            zstride = pl.zstride;
+        }
     if (!known) {
         std::vector<pbg_window> hw(n_win);
         HIPCHK(c, hipMemcpyAsync(hw.data(), wins, n_win * sizeof(pbg_window), hipMemcpyDeviceToHost,
                                  (hipStream_t)stream));
         HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
-        uint64_t worst = 0;
+        uint64_t worst = 0, maxlen = 0;
         for (uint32_t i = 0; i < n_win; ++i) {
             if (hw[i].beg < 0 || hw[i].end < hw[i].beg || (uint32_t)hw[i].end > n_rows)
                 return fail(c, PBG_E_RANGE, "window outside the row range");
             const uint64_t len = (uint64_t)(hw[i].end - hw[i].beg);
+            maxlen = std::max(maxlen, len);
             // words: masks are mw words each (two for 16-byte rows)
             if (ld_ws || len > (uint64_t)pbg::kSegCap) worst += mw * len + (uint64_t)n * (len / 64 + 1) + (ld_ws ? mw * np * len : 0);
             if (o->stats & PBG_S_ZNS) worst += mw * np * len;
@@ -470,8 +477,24 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
             HIPCHK(c, hipMalloc((void **)&c->d_segcnt, segcnt_bytes));
             c->segcnt_cap = segcnt_bytes;
         }
+        // ZnS lists at fixed places (no pool allocation in the kernel) when windows are of
+        // (nearly) one length: n_win * npops * maxlen words, at most twice the exact need
+        if (o->stats & PBG_S_ZNS) {
+            uint64_t need = 0;
+            for (uint32_t i = 0; i < n_win; ++i) need += mw * np * (uint64_t)(hw[i].end - hw[i].beg);
+            const uint64_t zs = mw * np * std::max<uint64_t>(maxlen, 1);
+            if ((uint64_t)n_win * zs <= std::max<uint64_t>(2 * need, 1 << 20) && (uint64_t)n_win * zs <= kPoolMax) {
+                zstride = zs;
+                if ((uint64_t)n_win * zs * 8 > c->zns_cap) {
+                    if (c->d_zns) HIPCHK(c, hipFree(c->d_zns));
+                    c->d_zns = nullptr;
+                    HIPCHK(c, hipMalloc((void **)&c->d_zns, (size_t)n_win * zs * 8));
+                    c->zns_cap = (size_t)n_win * zs * 8;
+                }
+            }
+        }
         if (c->plans.size() >= 16) c->plans.erase(c->plans.begin());
-        c->plans.push_back({wins, n_win, n_rows, o->stats});
+        c->plans.push_back({wins, n_win, n_rows, o->stats, zstride});
     }
     A.pool = c->d_ws;
     A.pool_cap = c->ws_cap / 8;
@@ -480,6 +503,8 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     A.pool_used = reinterpret_cast<unsigned long long *>(c->d_wsoff + 2 * (size_t)n_win + (size_t)n_win * np);
     A.err = c->d_err;
     HIPCHK(c, hipMemsetAsync(A.pool_used, 0, 8, (hipStream_t)stream));
+    A.zlist = c->d_zns;
+    A.zstride = zstride;
     A.seg_count = c->d_segcnt;
     A.var_count = c->d_segcnt + n_win;
     A.ld_ns = c->d_segcnt + n_win + (size_t)n_win * np;

@@ -163,7 +163,11 @@ struct StatsArgs {
     unsigned long long *pool_used;        // [1] words taken, zeroed per call
     int *err;
     uint64_t *win_off;                    // [2*n_win] pool offsets: seg rows, omega / Wall lists
-    uint64_t *zoff;                       // [n_win*npops] pool offset of each ZnS chain's list
+    uint64_t *zoff;                       // [n_win*npops] offset of each ZnS chain's list (pool or zlist)
+    // ZnS lists at fixed places when the window lengths allow it (zstride > 0): window w,
+    // population i at zlist + w * zstride + i * (zstride / npops); else bump-allocated in the pool
+    uint64_t *zlist;
+    uint64_t zstride;                     // u64 words per window
     int32_t *seg_count;                   // [n_win] segregating rows
     int32_t *var_count;                   // [n_win*npops] ZnS: rows variable within the population
     int32_t *ld_ns;                       // [n_win*npops] ZnS: the reference's num_snps

@@ -421,7 +421,40 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     // segregating rows variable within it (masked to the population) goes to the pool for
     // window_zns_kernel, with num_snps (variable sites among the first S-1, plus the final
     // unconditional increment)
-    if (stats & PBG_S_ZNS) {
+    if ((stats & PBG_S_ZNS) && A.zstride) {
+        // lists at fixed places: one pass per population writes the list and counts it
+        const uint64_t zreg = A.zstride / (uint64_t)np;   // words per population region
+        for (int i = 0; i < np; ++i) {
+            const M pm = pop_mask<M>(P, i);
+            const int nn = P.pop_n[i], mf = A.min_freq;
+            const uint64_t off = (uint64_t)w * A.zstride + (uint64_t)i * zreg;
+            M *vl = reinterpret_cast<M *>(A.zlist + off);
+            uint32_t V = 0;
+            int lastvar = 0;
+            for (uint32_t c0 = 0; c0 < S; c0 += 64) {
+                const uint32_t j = c0 + (uint32_t)lane;
+                M t{};
+                bool v = false;
+                if (j < S) {
+                    t = seg_at(j) & pm;
+                    const int m = (int)pc(t);
+                    v = m >= mf && m <= nn - mf;
+                    if (j == S - 1) lastvar = v ? 1 : 0;
+                }
+                const uint64_t bm = __ballot(v);
+                if (v) vl[V + (uint32_t)__popcll(bm & ((1ULL << lane) - 1))] = t;
+                V += (uint32_t)__popcll(bm);
+            }
+            // num_snps: variable sites among the first S-1, plus the final increment
+            if (lane == (S ? (int)((S - 1) & 63u) : 0)) {   // the lane that saw row S-1 knows lastvar
+                const int ns = S >= 1 ? (int)V - lastvar + 1 : 0;
+                A.var_count[(size_t)w * np + i] = (int)V;
+                A.zoff[(size_t)w * np + i] = off;
+                A.ld_ns[(size_t)w * np + i] = ns;
+                if (O.ld_snps) O.ld_snps[(size_t)w * np + i] = ns;
+            }
+        }
+    } else if (stats & PBG_S_ZNS) {
         // counts first (one pool allocation per window), then the lists
         uint32_t tot = 0;
         for (int i = 0; i < np; ++i) {
@@ -763,7 +796,7 @@ __global__ __launch_bounds__(64) void window_zns_kernel(DevParams P, DevTables T
         const uint32_t w = ch / (uint32_t)np;
         const int i = (int)(ch - w * (uint32_t)np);
         V = A.var_count[ch];
-        L = reinterpret_cast<const M *>(A.pool + A.zoff[ch]);
+        L = reinterpret_cast<const M *>((A.zstride ? A.zlist : A.pool) + A.zoff[ch]);
         np1 = P.pop_n[i] + 1;
         r2o = T.r2_off[i];
     }
@@ -874,7 +907,7 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
         const uint32_t w = ch / (uint32_t)np;
         const int i = (int)(ch - w * (uint32_t)np);
         V = A.var_count[ch];
-        L = reinterpret_cast<const M *>(A.pool + A.zoff[ch]);
+        L = reinterpret_cast<const M *>((A.zstride ? A.zlist : A.pool) + A.zoff[ch]);
         np1 = P.pop_n[i] + 1;
         r2o = T.r2_off[i];
     }

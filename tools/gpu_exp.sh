@@ -1,14 +1,6 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
-export TMPDIR=/tmp
-for v in base skipz skipzs skipzsn; do
-  rm -rf gpurun_out/prof_v
-  POPBAM_GPU_LIB=$R/popbam_amd/variants/$v/libpopbam_gpu.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$R/gpurun_out/prof_v" -o run \
-    -- python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/prof_v.log 2>&1 || exit 1
-  python3 -c "
-import csv
-for r in csv.DictReader(open('gpurun_out/prof_v/run_kernel_stats.csv')):
-    if r['Name'].startswith('window'): print('$v', r['Name'][:28], round(float(r['AverageNs'])/1e3, 1), 'us')
-"
-done
+BENCH_ARGS="--steps 10 --warmup 2 --cpu-sample 0" bash tools/ab.sh head zfix head zfix || exit 1
+timeout -k 10 700 python -u -m pytest -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_scale.py tests/test_gpu_golden.py tests/test_wide_samples.py tests/test_genome.py tests/test_cli.py > gpurun_out/pytest_stats.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_stats.log; exit 1; }
+tail -2 gpurun_out/pytest_stats.log
