@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--contigs", type=int, default=24, help="config 3: contigs")
     ap.add_argument("--contig-len", type=int, default=125_000_000, help="config 3: positions per contig")
     ap.add_argument("--chunk", type=int, default=1 << 25, help="config 3: positions per streamed pileup chunk")
+    ap.add_argument("--overlap", action="store_true",
+                    help="configs[3]/[4]: generate chunk c+1 on a second stream beside the call of chunk c "
+                         "(default: generate then call on one stream, so the call kernels run alone)")
     ap.add_argument("--pieces", type=int, default=1,
                     help="config 2: the contig's call in this many pieces (window borders), each piece's "
                          "statistics on a second stream beside the next piece's call (1 = call, then statistics)")
@@ -149,7 +152,7 @@ def cpu_baseline(args):
     if args.config == 4 or not ref_baseline.available():   # the reference cannot hold 96 samples
         return port
     L, n = args.ref_sample, args.samples
-    d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_{args.seed:x}_{L}_{n}", args.seed, L, n)
+    d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_v3_{args.seed:x}_{L}_{n}", args.seed, L, n)
     procs = max(1, min(16, os.cpu_count() or 1))
     t = ref_baseline.time_reference(d, L, args.window, procs)
     out = {"value": round(L / t["single_total_s"] / 1e6, 6), "unit": "Msites/s", "cores": 1, "kind": "reference",
@@ -189,6 +192,16 @@ def pcie_rate(torch, batch_bytes: int, step_s: float, sites: int) -> dict:
             "Msites_per_s_overlapped": round(sites / max(copy_s, step_s) / 1e6, 2)}
 
 
+def max_over_ranks(dist, x: float) -> float:
+    """The slowest rank's time (gloo, on the host)."""
+    if not dist:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def bench_genome(args, torch, dist, world, rank):
     """configs[3]: the whole synthetic genome (contigs x contig-len, 24 samples) streamed through
     HBM in double-buffered pileup chunks (popbam_amd.genome), contig-first shards across ranks,
@@ -199,13 +212,8 @@ def bench_genome(args, torch, dist, world, rank):
     n = args.samples
     ctx = _lib.Context(workload.default_params(n), torch.cuda.current_device())
     lengths = [args.contig_len] * args.contigs
-    if args.config == 4:   # overlapping windows: contiguous window blocks per rank, halo included
-        segs = genome.plan_overlapping(args.contig_len, world, args.window, args.step)[rank]
-        stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_HAP_EHHS
-    else:
-        segs = genome.plan_genome(lengths, world, args.window)[rank]
-        stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS | _lib.PBG_S_DIV_IND
-    gp = genome.GenomePass(ctx, segs, args.seed, args.depth, args.window, stats, args.chunk)
+    segs, stats = genome.rank_plan(args.config, lengths, world, rank, args.window, args.step)
+    gp = genome.GenomePass(ctx, segs, args.seed, args.depth, args.window, stats, args.chunk, serial=not args.overlap)
     for _ in range(args.warmup):
         gp.run()
     gp.synchronize()
@@ -221,11 +229,7 @@ def bench_genome(args, torch, dist, world, rank):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
     kt, kn = C.c_double(0.0), C.c_uint32(0)
     ctx.check(ctx.lib.pbg_kernel_time(ctx.h, C.byref(kt), C.byref(kn)), "pbg_kernel_time")
     ct, cn = C.c_double(0.0), C.c_uint32(0)
@@ -254,7 +258,7 @@ def bench_genome(args, torch, dist, world, rank):
     ctx.check(ctx.lib.pbg_kernel_time(ctx.h, C.byref(k1), C.byref(n1)), "pbg_kernel_time")
     ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
     scan_ms_alone = k1.value / max(1, n1.value)
-    achieved = sb0 / (scan_ms_alone * 1e-3) / 1e9
+    achieved_alone = sb0 / (scan_ms_alone * 1e-3) / 1e9
     out = None
     if rank == 0:
         value = total_sites * args.steps / elapsed / 1e6
@@ -273,22 +277,27 @@ def bench_genome(args, torch, dist, world, rank):
                        "genome_sites": total_sites, "sites_rank0": my_sites, "samples": n, "mean_depth": args.depth,
                        "window": args.window, "windows_rank0": gp.n_windows, "chunk_sites": args.chunk,
                        "chunks_rank0": chunks, "parallelism": f"dp{world} (contig-first shards, no collective)"},
-            "roofline": {"bound": "hbm", "kernel": "call_scan_kernel", "achieved": round(achieved, 2),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "bytes_per_launch": sb0, "ms_per_launch": round(scan_ms_alone, 4),
+            "roofline": {"bound": "hbm", "kernel": "call_scan_kernel", "achieved": round(achieved_pass, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_pass / HBM_PEAK_GBS, 4),
+                         "traffic": None, "bytes_per_launch": sb // max(1, chunks), "ms_per_launch": round(scan_ms, 4),
                          "bytes_basis": "SURVEY 8(d): sum over (position, sample) of 2k+5, +1 +row_bytes per position",
-                         "measured_on": "chunk 0 resident in HBM, 5 launches with nothing else on the GPU",
-                         "in_pass": {"ms_per_launch": round(scan_ms, 4), "achieved": round(achieved_pass, 2),
-                                     "frac": round(achieved_pass / HBM_PEAK_GBS, 4),
-                                     "note": "the same kernel inside the timed pass, sharing the CUs with the "
-                                             "next chunk's generator kernels"}},
+                         "measured_on": (f"every chunk launch of the timed pass ({chunks} per pass; library HIP "
+                                         "events on the call stream)") +
+                                        (", the next chunk's generator running beside it" if args.overlap else
+                                         ", each chunk generated before its call on the same stream"),
+                         "alone": {"ms_per_launch": round(scan_ms_alone, 4), "achieved": round(achieved_alone, 2),
+                                   "frac": round(achieved_alone / HBM_PEAK_GBS, 4), "bytes_per_launch": sb0,
+                                   "note": "chunk 0 resident in HBM, 5 launches with nothing else on the GPU"}},
             "call_stage": {"ms_per_pass": round(call_ms_pass, 3), "bytes_per_pass": sb,
                            "GBps": round(sb / (call_ms_pass * 1e-3) / 1e9, 2) if call_ms_pass else None,
                            "Msites_per_s_call_only": round(my_sites / (call_ms_pass * 1e-3) / 1e6, 2) if call_ms_pass else None},
             "note": "value includes the on-device generation of every pileup chunk (the input does not fit "
                     "HBM: ~1.8 TB of keys); call_stage is the call kernels alone (library HIP events)",
+            "pass_mode": "overlapped (two streams)" if args.overlap else "serial (generate, then call, per chunk)",
         }
         out["cpu_baseline"] = cpu_baseline(args) if (world == 1 and args.cpu_sample > 0) else None
+        if out["cpu_baseline"]:
+            out["x_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
     ctx.close()
 
@@ -302,9 +311,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
+        # gloo (host) for the timing barrier and the max over ranks: the data path has no
+        # collective, so RCCL is never initialised
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
 
@@ -350,11 +361,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
     kt, kn = C.c_double(0.0), C.c_uint32(0)
     ctx.check(ctx.lib.pbg_kernel_time(ctx.h, C.byref(kt), C.byref(kn)), "pbg_kernel_time")
     ct, cn = C.c_double(0.0), C.c_uint32(0)

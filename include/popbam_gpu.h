@@ -249,7 +249,10 @@ int pbg_call_time(pbg_ctx *ctx, double *ms_total, uint32_t *launches);
  * depth ~ Binomial(2 * mean_depth, 1/2), baseQ 20..40, mapQ 60, ~0.8 % error bases, theta
  * ~1.2 %), written straight into device memory in the pbg_pileup layout with the context's
  * filters applied (the keys the host side of the callback would have built).  Positions
- * [pos0, pos0 + n_sites) of `contig`; block_off is relative to this batch.                  */
+ * [pos0, pos0 + n_sites) of `contig`; block_off is relative to this batch.  A task's reads
+ * are a window of a per-seed table of 2^20 random read templates (built on the first call
+ * with a seed, which then synchronises `stream` once).  ref / k / rmsq / keys must be 16-byte
+ * aligned.                                                                                  */
 typedef struct {
     uint64_t seed;
     int32_t  contig;

@@ -1168,6 +1168,27 @@ uint64_t sm64(uint64_t x) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
+uint32_t mx32(uint32_t x) {   // lowbias32
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+// per (position, sample) hash and depth draw (pbg_common.h synth_sample_hash / synth_depth)
+uint64_t sample_hash(uint64_t h, int s) {
+    const uint32_t m = (uint32_t)(s + 1);
+    return (uint64_t)mx32((uint32_t)h ^ (m * 0xD1B54Bu)) | ((uint64_t)mx32((uint32_t)(h >> 32) ^ (m * 0x9E3779u)) << 32);
+}
+int depth_draw(uint64_t hs, int mean_depth) {
+    const int nb = 2 * mean_depth;
+    const uint32_t b0 = mx32((uint32_t)hs ^ 0x5851F42Du);
+    if (nb <= 32) return __builtin_popcount(b0 & (nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u)));
+    const uint32_t b1 = mx32((uint32_t)(hs >> 32) ^ 0x4C957F2Du);
+    const uint64_t m = nb >= 64 ? ~0ULL : ((1ULL << nb) - 1);
+    return __builtin_popcountll(((uint64_t)b0 | ((uint64_t)b1 << 32)) & m);
+}
 }  // namespace
 
 extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int32_t n, int32_t mean_depth,
@@ -1178,20 +1199,20 @@ extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int3
     int snp = ((h >> 2) & 0x3FF) < 12;
     int alt = (ref_idx + 1 + (int)((((h >> 12) & 0xFFFFu) * 3u) >> 16)) & 3;
     uint32_t f16 = (uint32_t)((h >> 16) & 0xFFFF);
+    const uint32_t tseed = (uint32_t)sm64(seed ^ 0x6A09E667F3BCC909ULL);   // read-template table seed
     *ref = (uint8_t)"ACGT"[ref_idx];
     uint32_t nr = 0;
     for (int s = 0; s < n; ++s) {
-        uint64_t hs = sm64(h ^ (0xD1B54A32D192ED03ULL * (uint64_t)(s + 1)));
-        uint64_t bits = sm64(hs ^ 0x5851F42D4C957F2DULL);
-        int nb = 2 * mean_depth;
-        uint64_t m = nb >= 64 ? ~0ULL : ((1ULL << nb) - 1);
-        int d = __builtin_popcountll(bits & m);
+        uint64_t hs = sample_hash(h, s);
+        int d = depth_draw(hs, mean_depth);
         if (d > max_depth) d = max_depth;   // call_base keeps the first max_depth reads (popbam.cpp:241-246)
         depth[s] = (uint16_t)d;
         int a0 = (snp && (uint32_t)(hs & 0xFFFF) < f16) ? alt : ref_idx;
         int a1 = (snp && (uint32_t)((hs >> 16) & 0xFFFF) < f16) ? alt : ref_idx;
+        // reads = template entries [o, o + d) (pbg_common.h synth_tmpl_*)
+        const uint32_t o = (uint32_t)((hs >> 32) & ((1u << 17) - 1)) * 8u;
         for (int r = 0; r < d; ++r) {
-            uint32_t hr = (uint32_t)(hs >> 32) ^ (0x9E3779B9u * (uint32_t)(r + 1));   // mix32 (lowbias32)
+            uint32_t hr = tseed ^ (0x9E3779B9u * (o + (uint32_t)r + 1u));   // mix32 (lowbias32)
             hr ^= hr >> 16;
             hr *= 0x7FEB352Du;
             hr ^= hr >> 15;
@@ -1236,7 +1257,7 @@ extern "C" void orc_synth_genotypes(uint64_t seed, int32_t contig, uint64_t pos_
         uint32_t f16 = (uint32_t)((h >> 16) & 0xFFFF);
         ref[i] = (uint8_t)"ACGT"[ref_idx];
         for (int s = 0; s < n; ++s) {
-            uint64_t hs = sm64(h ^ (0xD1B54A32D192ED03ULL * (uint64_t)(s + 1)));
+            uint64_t hs = sample_hash(h, s);
             int a0 = (snp && (uint32_t)(hs & 0xFFFF) < f16) ? alt : ref_idx;
             int a1 = (snp && (uint32_t)((hs >> 16) & 0xFFFF) < f16) ? alt : ref_idx;
             alleles[(size_t)i * n + s] = (uint8_t)(a0 | (a1 << 2));

@@ -87,7 +87,10 @@ def run(cmd: str, argv: list[str], device: int = 0, rank: int = 0, world: int = 
         refs = bam.refs
         names, lengths = [r[0] for r in refs], [r[1] for r in refs]
         tid, beg, end = opt.parse_region(o.region, names, lengths)
-        seq = feed.fasta_fetch(o.reffile, names[tid])
+        try:
+            seq = feed.fasta_fetch(o.reffile, names[tid])
+        except feed.FeedError as e:
+            raise opt.PopbamError(f"Failed to load index for fastA reference file: {o.reffile}: {e}") from e
         if len(seq) < end:   # positions past the contig's sequence: no reference base
             seq = seq + b"N" * (end - len(seq))
         fallback = 0 if not sm.rg2sample else -1
@@ -107,7 +110,7 @@ def run(cmd: str, argv: list[str], device: int = 0, rank: int = 0, world: int = 
             lo, hi = shard.positions_needed(reg[0], reg[1], o.win_size, windowed)
             chunk = max(1 << 16, -(-(hi - lo) // max(1, 4 * threads)))
             try:
-                return lo, bam.pileup_keys(tid, lo, hi, seq, sm.rg2sample, sm.n, o.max_depth, flt, fallback,
+                return lo, bam.pileup_keys(tid, lo, hi, seq, sm.rg2sample, sm.n, engine.max_depth_of(o), flt, fallback,
                                            threads=threads, chunk=chunk, win=o.win_size if windowed else 0)
             except feed.FeedError as e:
                 if e.code == feed.PBF_E_RG:
@@ -155,6 +158,8 @@ def _run_rank(cmd: str, argv: list[str]) -> int:
             res = (0, run(cmd, argv, device=dev, rank=rank, world=world))
         except opt.PopbamError as e:
             res = (1, str(e))
+        except Exception as e:   # any failure (GPU, feeder, ...) still reaches the gather
+            res = (1, f"rank {rank}: {type(e).__name__}: {e}")
         parts = [None] * world if rank == 0 else None
         dist.gather_object(res, parts, dst=0)
     finally:

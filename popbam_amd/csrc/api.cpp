@@ -19,6 +19,7 @@
 
 struct pbg_ctx {
     int device = 0;
+    int n_cu = 256;   // the device's CU count (persistent queue-kernel grid)
     pbg_params params{};
     pbg::DevParams dp{};
     pbg::DevTables dt{};
@@ -51,9 +52,11 @@ struct pbg_ctx {
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev, evc;
     size_t ev_used = 0;
-    // pbg_synth_pileup: block-total scan scratch
+    // pbg_synth_pileup: block-total scan scratch; read-template tables per seed (built once,
+    // never rebuilt while a generator launch on another stream may read them)
     uint64_t *d_synth = nullptr;
     size_t synth_cap = 0;
+    std::vector<std::pair<uint64_t, uint16_t *>> tmpl;
     // pbg_run text kept when the caller's buffer was too small (pbg_take_text)
     std::string text;
     // second stream for the deep-task queue kernel beside the shallow one (pbg_call_sites)
@@ -137,7 +140,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     if (p->n_samples < 1 || p->n_samples > PBG_MAX_SAMPLES)
         return fail(nullptr, PBG_E_ARG, "n_samples must be in [1, 126]");
     if (p->n_pops < 1 || p->n_pops > PBG_MAX_POPS) return fail(nullptr, PBG_E_ARG, "n_pops must be in [1, 64]");
-    if (p->max_depth < 1 || p->max_depth > 65535) return fail(nullptr, PBG_E_ARG, "max_depth must be in [1, 65535]");
+    if (p->max_depth < 0 || p->max_depth > 65535) return fail(nullptr, PBG_E_ARG, "max_depth must be in [0, 65535]");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return fail(nullptr, PBG_E_NODEV, "no HIP device visible (libpopbam_gpu has no CPU path)");
@@ -185,6 +188,9 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     };
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return bad(e, "hipSetDevice");
+    if ((e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
+        return bad(e, "hipDeviceGetAttribute");
+    if (c->n_cu < 1) c->n_cu = 1;
     std::vector<double> fk, beta, lhet;
     pbg::build_errmod_tables(fk, beta, lhet);
     // the scan's reference-only shortcut needs every beta[q][n][c < n] > 0 (q >= 4, n <= PBG_FAST_MAX)
@@ -268,6 +274,7 @@ void pbg_destroy(pbg_ctx *c) {
                     (void *)c->deep.blk_cnt, (void *)c->deep.raw,
                     (void *)c->d_segcnt, (void *)c->d_synth})
         if (p) (void)hipFree(p);
+    for (auto &t : c->tmpl) (void)hipFree(t.second);
     for (auto *v : {&c->ev, &c->evc})
         for (auto &e : *v) {
             (void)hipEventDestroy(e.first);
@@ -354,7 +361,7 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
     }
     const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys};
     HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, B, cap, rows, cb, c->d_err, c->deep,
-                                     (hipStream_t)stream, e0, e1, c->aux, c->ev_scan, c->ev_deep));
+                                     (hipStream_t)stream, e0, e1, c->aux, c->ev_scan, c->ev_deep, c->n_cu));
     if (c1) HIPCHK(c, hipEventRecord(c1, (hipStream_t)stream));
     return PBG_OK;
 }
@@ -524,9 +531,21 @@ int pbg_synth_pileup(pbg_ctx *c, const pbg_synth_spec *sp, uint8_t *ref, void *k
                      uint16_t *keys, uint64_t keys_cap, uint64_t *n_keys, void *stream) {
     if (!c || !sp || !ref || !k || !rmsq || !block_off || (!keys && keys_cap)) return fail(c, PBG_E_ARG, "null argument");
     if (sp->mean_depth < 1 || sp->mean_depth > 32) return fail(c, PBG_E_ARG, "mean_depth must be in [1, 32]");
-    if ((uintptr_t)keys & 15) return fail(c, PBG_E_ARG, "keys must be 16-byte aligned");
+    if (((uintptr_t)keys | (uintptr_t)k | (uintptr_t)rmsq | (uintptr_t)ref) & 15)
+        return fail(c, PBG_E_ARG, "keys / k / rmsq / ref must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
+    const uint16_t *tmpl = nullptr;
+    for (auto &t : c->tmpl)
+        if (t.first == sp->seed) tmpl = t.second;
+    if (!tmpl) {   // first use of this seed: build its table and wait for it (every stream may read it)
+        uint16_t *t = nullptr;
+        HIPCHK(c, hipMalloc((void **)&t, pbg::kTmplSize * sizeof(uint16_t)));
+        c->tmpl.emplace_back(sp->seed, t);
+        HIPCHK(c, pbg::launch_synth_tmpl(sp->seed, t, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        tmpl = t;
+    }
     const size_t need = pbg::synth_scratch_words(sp->n_sites) * 8;
     if (need > c->synth_cap) {
         if (c->d_synth) HIPCHK(c, hipFree(c->d_synth));
@@ -535,7 +554,7 @@ int pbg_synth_pileup(pbg_ctx *c, const pbg_synth_spec *sp, uint8_t *ref, void *k
         c->synth_cap = need;
     }
     HIPCHK(c, pbg::launch_synth(c->dp, sp->seed, sp->contig, sp->mean_depth, sp->pos0, sp->n_sites, ref, k, rmsq,
-                                block_off, keys, keys_cap, c->d_synth, c->d_err, s));
+                                block_off, keys, keys_cap, c->d_synth, tmpl, c->d_err, s));
     if (n_keys) {
         const uint32_t nblk = (sp->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
         HIPCHK(c, hipMemcpyAsync(n_keys, block_off + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost, s));

@@ -100,17 +100,7 @@ __host__ __device__ inline SynthSite synth_site(uint64_t seed, int contig, uint6
     s.f16 = (uint32_t)((s.h >> 16) & 0xFFFF);   // derived allele frequency
     return s;
 }
-__host__ __device__ inline uint64_t synth_sample_hash(const SynthSite &s, int sample) {
-    return splitmix64(s.h ^ (0xD1B54A32D192ED03ULL * (uint64_t)(sample + 1)));
-}
-__host__ __device__ inline int synth_depth(uint64_t hs, int mean_depth) {
-    // binomial(2D, 1/2): popcount of 2D random bits (mean D), D <= 32
-    uint64_t bits = splitmix64(hs ^ 0x5851F42D4C957F2DULL);
-    int nb = 2 * mean_depth;
-    uint64_t m = nb >= 64 ? ~0ULL : ((1ULL << nb) - 1);
-    return __builtin_popcountll(bits & m);
-}
-// 32-bit finaliser (lowbias32) for the per-read draws: one per read, ~4x cheaper than splitmix64
+// 32-bit finaliser (lowbias32): two 32-bit multiplies, ~4x cheaper than splitmix64's 64-bit ones
 __host__ __device__ inline uint32_t mix32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7FEB352Du;
@@ -119,18 +109,58 @@ __host__ __device__ inline uint32_t mix32(uint32_t x) {
     x ^= x >> 16;
     return x;
 }
-__host__ __device__ inline uint32_t synth_read(const SynthSite &s, uint64_t hs, int r) {
-    int a0 = (s.snp && (uint32_t)(hs & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
-    int a1 = (s.snp && (uint32_t)((hs >> 16) & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
-    // read r's 32 random bits: haplotype (bit 0), error (bits 1-7 all zero: 1/128), error base
-    // (bits 8-15), baseQ (bits 16-31), strand (bit 8 ^ bit 17)
-    const uint32_t hr = mix32((uint32_t)(hs >> 32) ^ (0x9E3779B9u * (uint32_t)(r + 1)));
-    int base = (hr & 1) ? a1 : a0;
-    // ~0.8 % errors; fixed-point ranges (no division): other base 1..3 steps away, baseQ 20..40
-    if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((((hr >> 8) & 0xFFu) * 3u) >> 8)) & 3;
-    const uint32_t bq = 20 + ((((hr >> 16) & 0xFFFFu) * 21u) >> 16);
+// per (position, sample): 64 bits from the two halves of the site hash, each keyed on the sample
+// by a 24-bit constant (the multiply is a full-rate v_mul_u32_u24: (sample + 1) * K < 2^31)
+__host__ __device__ inline uint64_t synth_sample_hash(const SynthSite &s, int sample) {
+    const uint32_t m = (uint32_t)(sample + 1);
+    const uint32_t lo = mix32((uint32_t)s.h ^ (m * 0xD1B54Bu));
+    const uint32_t hi = mix32((uint32_t)(s.h >> 32) ^ (m * 0x9E3779u));
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__host__ __device__ inline int synth_depth(uint64_t hs, int mean_depth) {
+    // binomial(2D, 1/2): popcount of 2D random bits (mean D), D <= 32
+    const int nb = 2 * mean_depth;
+    const uint32_t b0 = mix32((uint32_t)hs ^ 0x5851F42Du);
+    if (nb <= 32) return __builtin_popcount(b0 & (nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u)));
+    const uint32_t b1 = mix32((uint32_t)(hs >> 32) ^ 0x4C957F2Du);
+    const uint64_t m = nb >= 64 ? ~0ULL : ((1ULL << nb) - 1);
+    return __builtin_popcountll(((uint64_t)b0 | ((uint64_t)b1 << 32)) & m);
+}
+// The per-read draws come from a table of read templates (kTmplN + 64 entries, 2 MB as u16,
+// L2-resident): task (position, sample) reads entries [o, o + depth) with o = synth_tmpl_off(hs),
+// a multiple of 8, so the generator copies a task's reads with 16-byte loads.  Entry i:
+// bq << 5 | strand << 4 | hap << 2 | e, drawn from 32 random bits hr_i: haplotype (bit 0),
+// error (bits 1-7 all zero: 1/128) with the error base 1..3 steps away (e, from bits 8-15;
+// e = 0: no error), baseQ 20..40 (bits 16-31), strand (bit 8 ^ bit 17).  Fixed-point ranges, no
+// division.
+constexpr uint32_t kTmplN = 1u << 20;
+constexpr uint32_t kTmplSize = kTmplN + 64;   // the last task window may start at kTmplN - 8
+__host__ __device__ inline uint32_t synth_tmpl_seed(uint64_t seed) {
+    return (uint32_t)splitmix64(seed ^ 0x6A09E667F3BCC909ULL);
+}
+__host__ __device__ inline uint32_t synth_tmpl_entry(uint32_t tseed, uint32_t i) {
+    const uint32_t hr = mix32(tseed ^ (0x9E3779B9u * (i + 1u)));
+    const uint32_t e = ((hr >> 1) & 127u) == 0 ? 1u + ((((hr >> 8) & 0xFFu) * 3u) >> 8) : 0u;
+    const uint32_t bq = 20u + ((((hr >> 16) & 0xFFFFu) * 21u) >> 16);
     const uint32_t strand = ((hr >> 8) ^ (hr >> 17)) & 1u;
-    return bq | (60u << 8) | ((1u << base) << 16) | (strand << 20);
+    return (bq << 5) | (strand << 4) | ((hr & 1u) << 2) | e;
+}
+// first template entry of a task (bits 32..48 of its sample hash; the alleles use bits 0..31)
+__host__ __device__ inline uint32_t synth_tmpl_off(uint64_t hs) { return (uint32_t)((hs >> 32) & (kTmplN / 8 - 1)) * 8u; }
+// the task's two haplotype alleles a0 | a1 << 2
+__host__ __device__ inline uint32_t synth_alleles(const SynthSite &s, uint64_t hs) {
+    const int a0 = (s.snp && (uint32_t)(hs & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
+    const int a1 = (s.snp && (uint32_t)((hs >> 16) & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
+    return (uint32_t)(a0 | (a1 << 2));
+}
+// raw read word (bits 0-7 baseQ, 8-15 mapQ 60, 16-19 nt16 base, 20 strand) of a template entry
+__host__ __device__ inline uint32_t synth_tmpl_read(uint32_t ent, uint32_t alv) {
+    const uint32_t base = (((alv >> (2u * ((ent >> 2) & 1u))) & 3u) + (ent & 3u)) & 3u;
+    return (ent >> 5) | (60u << 8) | ((1u << base) << 16) | (((ent >> 4) & 1u) << 20);
+}
+// read r of a task
+__host__ __device__ inline uint32_t synth_read(const SynthSite &s, uint64_t hs, int r, uint32_t tseed) {
+    return synth_tmpl_read(synth_tmpl_entry(tseed, synth_tmpl_off(hs) + (uint32_t)r), synth_alleles(s, hs));
 }
 // every synthetic read survives call_base's filters: baseQ 20..40 (no Illumina offset), mapQ 60,
 // one-hot A/C/G/T bases
@@ -221,17 +251,19 @@ struct Batch {
 // kernel launchers (defined in call_kernel.hip / stats_kernel.hip)
 // aux (may be null): a second stream the deep-task queue kernel runs on, beside the shallow
 // one (they read disjoint queue ends); ev_scan / ev_deep order it after the scan and the fold
-// after it.
+// after it.  n_cu: the context device's CU count (sizes the persistent queue kernel's grid).
 hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, const Batch &B, uint32_t cap,
                              void *rows, uint64_t *cb, int *err, const struct DeepBufs &D, hipStream_t stream,
-                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, hipStream_t aux = nullptr,
-                             hipEvent_t ev_scan = nullptr, hipEvent_t ev_deep = nullptr);
+                             hipEvent_t ev0, hipEvent_t ev1, hipStream_t aux, hipEvent_t ev_scan, hipEvent_t ev_deep,
+                             int n_cu);
 size_t call_sites_lds_bytes(int n, uint32_t cap);
 // synthetic batch: k / rmsq / ref + per-block key totals, then an exclusive scan of the totals
 // into block_off (scratch: one u64 per 1024 blocks), then the keys
 hipError_t launch_synth(const DevParams &P, uint64_t seed, int contig, int mean_depth, int64_t pos0, uint32_t n_sites,
                         uint8_t *ref, void *k, uint32_t *rmsq, uint64_t *block_off, uint16_t *keys,
-                        uint64_t keys_cap, uint64_t *scratch, int *err, hipStream_t stream);
+                        uint64_t keys_cap, uint64_t *scratch, const uint16_t *tmpl, int *err, hipStream_t stream);
+// the read-template table of a seed (kTmplSize u16 entries, 16-byte aligned)
+hipError_t launch_synth_tmpl(uint64_t seed, uint16_t *tmpl, hipStream_t stream);
 size_t synth_scratch_words(uint32_t n_sites);
 hipError_t launch_window_stats(int row_bytes, const DevParams &P, const DevTables &T, const void *rows,
                                uint32_t n_rows, uint32_t n_win, const StatsArgs &A, hipStream_t stream);

@@ -151,16 +151,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
 
     const int n = P.n, np = P.npops;
     const int lane = threadIdx.x;
-#ifdef PBG_WIN_SKIP   // timing experiments only: statistics left out of this kernel
-    const uint32_t stats = A.stats & ~(uint32_t)(PBG_WIN_SKIP);
-    if ((A.stats & PBG_S_ZNS) && ((PBG_WIN_SKIP) & PBG_S_ZNS) && lane < np) {   // window_zns_kernel runs no chain
-        A.var_count[(size_t)w * np + lane] = 0;
-        A.zoff[(size_t)w * np + lane] = 0;
-        A.ld_ns[(size_t)w * np + lane] = 0;
-    }
-#else
     const uint32_t stats = A.stats;
-#endif
     const int64_t wb = A.wins[w].beg, we = A.wins[w].end > A.wins[w].beg ? A.wins[w].end : A.wins[w].beg;
     const bool ld_ws = (stats & (PBG_S_OMEGA | PBG_S_WALL)) != 0;  // window_ld_kernel reads the seg list
     for (int i = lane; i < L.r2lds; i += 64) s_r2[i] = T.r2[i];
@@ -280,16 +271,6 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         if (A.seg_count) A.seg_count[w] = (int)S;
     }
     const int npairs = np * (np - 1);
-#ifdef PBG_WIN_TIME_LOADS   // timing experiments only: the row pass alone
-    if (S < 1000000u) {   // no ZnS chains to run (window_zns_kernel reads var_count / zoff)
-        if ((stats & PBG_S_ZNS) && lane < np) {
-            A.var_count[(size_t)w * np + lane] = 0;
-            A.zoff[(size_t)w * np + lane] = 0;
-            A.ld_ns[(size_t)w * np + lane] = 0;
-        }
-        return;
-    }
-#endif
 
     // ---- bitplanes (hap.seq) and the u16 pairwise-difference matrix
     uint64_t *plane = nullptr;
@@ -421,9 +402,18 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     // segregating rows variable within it (masked to the population) goes to the pool for
     // window_zns_kernel, with num_snps (variable sites among the first S-1, plus the final
     // unconditional increment)
-    if ((stats & PBG_S_ZNS) && A.zstride) {
+    const uint64_t zreg = A.zstride / (uint64_t)np;   // ZnS list words per population region
+    if ((stats & PBG_S_ZNS) && A.zstride && (uint64_t)S * NW > zreg) {
+        // the plan's stride was sized for shorter windows (a window list changed in place):
+        // report it (pbg_check -> PBG_E_RANGE) instead of writing past the region
+        if (lane == 0) atomicOr(A.err, 4);
+        if (lane < np) {
+            A.var_count[(size_t)w * np + lane] = 0;
+            A.zoff[(size_t)w * np + lane] = 0;
+            A.ld_ns[(size_t)w * np + lane] = 0;
+        }
+    } else if ((stats & PBG_S_ZNS) && A.zstride) {
         // lists at fixed places: one pass per population writes the list and counts it
-        const uint64_t zreg = A.zstride / (uint64_t)np;   // words per population region
         for (int i = 0; i < np; ++i) {
             const M pm = pop_mask<M>(P, i);
             const int nn = P.pop_n[i], mf = A.min_freq;
@@ -756,135 +746,18 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
     if (O.ld_val) O.ld_val[(size_t)w * np + i] = x86nan(val);
 }
 
-// ZnS sums (calc_zns, pop_ld.cpp:215-248): a quad of lanes per (window, population) chain, 16
-// chains per wave.  The chain is the reference's exact sequence of additions over the pairs
-// a < b of the population's variable sites (a ascending, then b).  Each step the quad's four
-// lanes compute the r^2 of the next four pairs in parallel (the host's table, the reference's
-// own expression per (marg1, marg2, c11)), DPP quad broadcasts hand all four values to every
-// lane of the quad, and each lane adds them in pair order to the same running double -- so the
-// sum is bit-identical while the r^2 work runs 4-wide.  Pairs past the end add +0.0, which
-// leaves a sum of r^2 >= +0 unchanged.
-template <int K>
-__device__ __forceinline__ double quad_bcast(double x) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), K * 0x55, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), K * 0x55, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
 // list entries of a chain staged in LDS (longer lists: read from the pool), and the slot
 // stride: +16 B staggers the slots' LDS banks
 template <class M>
 constexpr int zns_stage() { return sizeof(M) == 8 ? 256 : 128; }
 template <class M>
 constexpr int zns_stride() { return zns_stage<M>() + (sizeof(M) == 8 ? 2 : 1); }
-constexpr int kZnsUnroll = 4;    // steps whose loads are issued before their adds (latency hiding)
-template <class M>
-__global__ __launch_bounds__(64) void window_zns_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A,
-                                                        int r2_lds) {
-    constexpr int kZnsStage = zns_stage<M>(), kZnsStride = zns_stride<M>();
-    extern __shared__ __align__(16) double s_dyn[];
-    double *s_r2t = s_dyn;                                                      // [r2_lds]
-    M *s_t = reinterpret_cast<M *>(s_dyn + r2_lds);                            // [16][kZnsStride] masks
-    for (int i = threadIdx.x; i < r2_lds; i += 64) s_r2t[i] = T.r2[i];
-    const int np = P.npops;
-    const int lane = threadIdx.x, g = lane & 3, q = lane >> 2;
-    const uint32_t nch = n_win * (uint32_t)np;
-    const uint32_t ch = blockIdx.x * 16 + (uint32_t)q;
-    int V = 0;
-    const M *L = reinterpret_cast<const M *>(A.pool);
-    int np1 = 1, r2o = 0;
-    if (ch < nch) {
-        const uint32_t w = ch / (uint32_t)np;
-        const int i = (int)(ch - w * (uint32_t)np);
-        V = A.var_count[ch];
-        L = reinterpret_cast<const M *>((A.zstride ? A.zlist : A.pool) + A.zoff[ch]);
-        np1 = P.pop_n[i] + 1;
-        r2o = T.r2_off[i];
-    }
-    // all chains of the wave staged in LDS, or all read from the pool (wave-uniform, so every
-    // load below has a known address space: ds_read, not flat)
-    const bool staged = !__ballot(V > kZnsStage);
-    M *lt = s_t + q * kZnsStride;
-    if (staged)
-        for (int j = g; j < V; j += 4) lt[j] = L[j];
-    __syncthreads();
-    // row a, pairs b = b0 + g (b0 = a+1, a+5, ...); lanes past the row end add +0.0.  Branch-free:
-    // every step's list loads depend only on the (a, b0) arithmetic, so the loads of all
-    // kZnsUnroll steps issue before the first add waits on them.
-    auto run = [&](const M *lst, const double *r2p) -> double {
-        const int vm1 = V > 0 ? V - 1 : 0;
-        int a = 0, b0 = 1;
-        double acc = 0.0;
-        while (__ballot(a < V - 1)) {   // wave-uniform: until every chain of the wave is done
-            int ia[kZnsUnroll], ib[kZnsUnroll];
-            bool ok[kZnsUnroll];
-#pragma unroll
-            for (int u = 0; u < kZnsUnroll; ++u) {
-                const int b = b0 + g;
-                ok[u] = (a < V - 1) & (b < V);
-                ia[u] = min(a, vm1);
-                ib[u] = min(b, vm1);
-                b0 += 4;
-                const bool nxt = (b0 >= V) & (a < V - 1);
-                a += nxt ? 1 : 0;
-                b0 = nxt ? a + 1 : b0;
-            }
-            double r[kZnsUnroll];
-#pragma unroll
-            for (int u = 0; u < kZnsUnroll; ++u) {
-                const M ta = lst[ia[u]], tb = lst[ib[u]];
-                const double rv = r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
-                r[u] = ok[u] ? rv : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < kZnsUnroll; ++u) {   // pair order: step u's four pairs, lane 0..3
-                const double v0 = quad_bcast<0>(r[u]), v1 = quad_bcast<1>(r[u]), v2 = quad_bcast<2>(r[u]),
-                             v3 = quad_bcast<3>(r[u]);
-                acc += v0;
-                acc += v1;
-                acc += v2;
-                acc += v3;
-            }
-        }
-        return acc;
-    };
-    double acc;
-    if (staged) acc = r2_lds ? run(lt, s_r2t + r2o) : run(lt, T.r2 + r2o);
-    else acc = r2_lds ? run(L, s_r2t + r2o) : run(L, T.r2 + r2o);
-    if (g == 0 && ch < nch) {
-        const uint32_t w = ch / (uint32_t)np;
-        double val = 0.0;
-        if (A.seg_count[w] >= 1) {
-            const int ns = A.ld_ns[ch];
-            val = acc * (2.0 / (ns * (ns - 1)));
-        }
-        if (A.out.ld_val) A.out.ld_val[ch] = x86nan(val);
-    }
-}
-
 // ZnS sums, 16 lanes per chain: each 16-lane row of a wave owns one (window, population)
 // chain; per step its lanes compute the r^2 of the next 16 pairs of the current row a (lanes
-// past the row's end give +0.0) and every lane of the row adds the 16 values in pair order
-// (DPP row_newbcast hands lane j's value to the whole row), so the chain is the reference's
-// exact sequence of additions with 16-wide r^2 work.  Four chains per wave, 16 per workgroup,
-// and four times the waves of the quad kernel above: the dependent adds of more chains
-// interleave on each SIMD.
-template <int J>
-__device__ __forceinline__ double row_bcast(double x) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x150 + J, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x150 + J, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
-template <int J>
-__device__ __forceinline__ void add_row(double &acc, double r) {
-    if constexpr (J < 16) {
-        acc += row_bcast<J>(r);
-        add_row<J + 1>(acc, r);
-    }
-}
-#ifndef PBG_ZNS_UNROLL
-#define PBG_ZNS_UNROLL 1   // steps per pipelined round (1: 0.37 ms of statistics at configs[2]; 2: 0.38; 4: 0.40)
-#endif
-constexpr int kZnsRowUnroll = PBG_ZNS_UNROLL;
+// past the row's end give +0.0) and the row's first lane adds the 16 values in pair order
+// (broadcast LDS reads), so the chain is the reference's exact sequence of additions with
+// 16-wide r^2 work.  Four chains per wave, 16 per workgroup.
+constexpr int kZnsRowUnroll = 1;   // steps per pipelined round (1: 0.37 ms of statistics at configs[2]; 2: 0.38; 4: 0.40)
 template <class M>
 __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A,
                                                              int r2_lds) {
@@ -917,86 +790,6 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
     if (staged)
         for (int j = g; j < V; j += 16) lt[j] = L[j];
     __syncthreads();
-    auto run = [&](const M *lst, const double *r2p) -> double {
-        const int vm1 = V > 0 ? V - 1 : 0;
-#ifndef PBG_ZNS_ROWSTEP
-        // Lane g holds pair 16s + g of the chain's flat pair sequence (rows a ascending, b
-        // ascending within a row): a step spans row ends, so only the chain's last step adds
-        // padding.  Pair (a, b) past its row's end (b >= V) moves to (a + 1, a + 2 + (b - V)).
-        int a = 0, b = 1 + g;
-        auto norm = [&]() {
-            while ((b >= V) & (a < V - 1)) {
-                b += a + 2 - V;
-                ++a;
-            }
-        };
-        norm();
-#else
-        int a = 0, b0 = 1;
-#endif
-        double acc = 0.0;
-        while (__ballot(a < V - 1)) {   // wave-uniform: until the wave's four chains are done
-            double r[kZnsRowUnroll];
-#pragma unroll
-            for (int u = 0; u < kZnsRowUnroll; ++u) {
-#ifndef PBG_ZNS_ROWSTEP
-                const bool ok = (a < V - 1) & (b < V);
-                const M ta = lst[min(a, vm1)], tb = lst[min(b, vm1)];
-                const double rv = r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
-                r[u] = ok ? rv : 0.0;
-                b += 16;
-                norm();
-#else
-                const int b = b0 + g;
-                const bool ok = (a < V - 1) & (b < V);
-                const M ta = lst[min(a, vm1)], tb = lst[min(b, vm1)];
-                const double rv = r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
-                r[u] = ok ? rv : 0.0;
-                b0 += 16;
-                const bool nxt = (b0 >= V) & (a < V - 1);
-                a += nxt ? 1 : 0;
-                b0 = nxt ? a + 1 : b0;
-#endif
-            }
-#ifdef PBG_ZNS_DPP
-#pragma unroll
-            for (int u = 0; u < kZnsRowUnroll; ++u) add_row<0>(acc, r[u]);   // pair order: lane 0..15
-#else
-            // the row's values through LDS: every lane of the row reads the same words (broadcast
-            // reads, two doubles each) and adds them in pair order
-#pragma unroll
-            for (int u = 0; u < kZnsRowUnroll; ++u) sv[16 * u + g] = r[u];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const double2 *sv2 = reinterpret_cast<const double2 *>(sv);
-#ifndef PBG_ZNS_ALL_LANES
-            // only the row's first lane keeps the sum (it writes the output): one active lane
-            // per row, so each broadcast read moves 4 lanes' words instead of the wave's 64
-            if (g == 0)
-#endif
-            {
-                // every read issued before the first add (sched_barrier): the adds then run back
-                // to back instead of each pair waiting on its own LDS round trip
-                double2 v[8 * kZnsRowUnroll];
-#pragma unroll
-                for (int x = 0; x < 8 * kZnsRowUnroll; ++x) v[x] = sv2[x];
-#ifndef PBG_ZNS_NO_AHEAD
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-#pragma unroll
-                for (int x = 0; x < 8 * kZnsRowUnroll; ++x) {
-                    acc += v[x].x;
-                    acc += v[x].y;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-#endif
-        }
-        return acc;
-    };
-#ifndef PBG_ZNS_NO_PIPE
     // Software-pipelined rounds: round i's values are read from one half of the chain's LDS
     // buffer while round i+1's r^2 values are produced into registers (their list / table loads
     // in flight during the reads, their VALU free to interleave with round i's dependent adds --
@@ -1057,11 +850,6 @@ __global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTab
     double acc;
     if (staged) acc = r2_lds ? run_pipe(lt, s_r2t + r2o) : run_pipe(lt, T.r2 + r2o);
     else acc = r2_lds ? run_pipe(L, s_r2t + r2o) : run_pipe(L, T.r2 + r2o);
-#else
-    double acc;
-    if (staged) acc = r2_lds ? run(lt, s_r2t + r2o) : run(lt, T.r2 + r2o);
-    else acc = r2_lds ? run(L, s_r2t + r2o) : run(L, T.r2 + r2o);
-#endif
     if (g == 0 && ch < nch) {
         const uint32_t w = ch / (uint32_t)np;
         double val = 0.0;
@@ -1095,21 +883,12 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
         const int r2_lds = r2_total <= 4608 ? r2_total : 0;   // <= 36 KB of LDS per wave
         const uint32_t chains = n_win * (uint32_t)P.npops;
         const dim3 g((chains + 15) / 16);
-#ifdef PBG_ZNS_QUAD
-        if (rb == 16)
-            hipLaunchKernelGGL(window_zns_kernel<M2>, g, dim3(64), (size_t)r2_lds * 8 + 16 * zns_stride<M2>() * 16, stream,
-                               P, T, n_win, A, r2_lds);
-        else
-            hipLaunchKernelGGL(window_zns_kernel<uint64_t>, g, dim3(64), (size_t)r2_lds * 8 + 16 * zns_stride<uint64_t>() * 8,
-                               stream, P, T, n_win, A, r2_lds);
-#else
         if (rb == 16)
             hipLaunchKernelGGL(window_zns_row_kernel<M2>, g, dim3(256), (size_t)r2_lds * 8 + 16 * zns_stride<M2>() * 16,
                                stream, P, T, n_win, A, r2_lds);
         else
             hipLaunchKernelGGL(window_zns_row_kernel<uint64_t>, g, dim3(256),
                                (size_t)r2_lds * 8 + 16 * zns_stride<uint64_t>() * 8, stream, P, T, n_win, A, r2_lds);
-#endif
     }
     const uint32_t ld = A.stats & (PBG_S_OMEGA | PBG_S_WALL);
     if (ld) {

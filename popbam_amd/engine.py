@@ -17,6 +17,17 @@ from . import feed
 from . import options as opt
 
 
+def max_depth_of(o: opt.Options) -> int:
+    """-x as call_base applies it (popbam.cpp:209-246): the first max_depth reads of a sample
+    are kept, so 0 keeps none (every sample fails qfilter's depth test unless -m 0).  The
+    pileup holds at most 8000 reads per position (bam_pileup.c:375), so every -x above 65535
+    (the k width the device stores) behaves like 65535.  A negative -x makes the reference's
+    read buffer allocation throw (new[] of a negative size); it is refused here instead."""
+    if o.max_depth < 0:
+        raise opt.PopbamError(f"maximum read depth -x {o.max_depth} must not be negative")
+    return min(o.max_depth, 65535)
+
+
 def make_params(o: opt.Options, sm: opt.SampleModel) -> _lib.PbgParams:
     masks, counts = sm.pop_masks()
     if len(masks) > _lib.PBG_MAX_POPS:
@@ -28,7 +39,7 @@ def make_params(o: opt.Options, sm: opt.SampleModel) -> _lib.PbgParams:
     for i, (m, c) in enumerate(zip(masks, counts)):
         p.set_pop_mask(i, m)
         p.pop_n[i] = c
-    p.min_depth, p.max_depth = o.min_depth, o.max_depth
+    p.min_depth, p.max_depth = o.min_depth, max_depth_of(o)
     p.min_rmsQ, p.min_snpQ = o.min_rmsQ, o.min_snpQ
     p.min_mapQ, p.min_baseQ = o.min_mapQ & 0xFF, o.min_baseQ & 0xFF
     p.flag = o.flag
@@ -37,7 +48,7 @@ def make_params(o: opt.Options, sm: opt.SampleModel) -> _lib.PbgParams:
 
 def make_filter(o: opt.Options):
     """call_base's per-read filters for the host side of the callback (popbam.cpp:266-281)."""
-    return feed.make_filter(o.min_baseQ, o.min_mapQ, o.flag, o.max_depth)
+    return feed.make_filter(o.min_baseQ, o.min_mapQ, o.flag, max_depth_of(o))
 
 
 class _Cmd:

@@ -91,16 +91,31 @@ def plan_overlapping(length: int, world: int, win: int, step: int) -> list[list[
     return plan
 
 
+def rank_plan(config: int, lengths: list[int], world: int, rank: int, win: int, step: int = 0):
+    """A rank's segments and statistics for BASELINE configs[3] (contig-first shards of the
+    whole genome: nucdiv + sfs + ld ZnS + diverge) or configs[4] (one contig, overlapping
+    windows in contiguous blocks with their halo: nucdiv + sfs + haplo EHHS)."""
+    if config == 4:
+        return (plan_overlapping(lengths[0], world, win, step)[rank],
+                _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_HAP_EHHS)
+    return (plan_genome(lengths, world, win)[rank],
+            _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS | _lib.PBG_S_DIV_IND)
+
+
 class GenomePass:
     """Streams the synthetic pileup of `segments` through the call kernels chunk by chunk
     (double-buffered, producer and call on separate streams) into genome-resident rows, then
     runs the window statistics per segment.  One `run()` = one pass over every position."""
 
     def __init__(self, ctx: _lib.Context, segments: list[Segment], seed: int, mean_depth: int = 10,
-                 win: int = 10_000, stats: int = 0, chunk: int = 1 << 25, device: str = "cuda"):
+                 win: int = 10_000, stats: int = 0, chunk: int = 1 << 25, device: str = "cuda",
+                 serial: bool = False):
         assert chunk % SITE_BLOCK == 0
         self.ctx, self.segments, self.seed, self.mean_depth, self.win = ctx, segments, seed, mean_depth, win
         self.stats, self.chunk = stats, chunk
+        # serial: each chunk is generated on the call stream right before its call (the call's
+        # kernels then have the GPU to themselves); else double-buffered on two streams
+        self.serial = serial
         rb = ctx.row_bytes
         # rows: one region per segment, each starting 16-byte aligned
         self.row_base = []
@@ -124,7 +139,7 @@ class GenomePass:
                          rmsq=torch.empty(chunk * n, dtype=torch.int32, device=device),
                          block_off=torch.zeros(nblk + 1, dtype=torch.int64, device=device),
                          keys=torch.empty(max(8, self.keys_cap), dtype=torch.int16, device=device))
-                    for _ in range(2)]
+                    for _ in range(1 if serial else 2)]
         self.key_total = torch.zeros(1, dtype=torch.int64, device=device)   # keys called (SURVEY 8(d) bytes)
         self.gen_stream = torch.cuda.Stream(device=device)
         self.call_stream = torch.cuda.Stream(device=device)
@@ -164,15 +179,15 @@ class GenomePass:
     def n_sites(self) -> int:
         return sum(s.end - s.beg for s in self.segments)
 
-    def _generate(self, c: int, slot: int):
+    def _generate(self, c: int, slot: int, stream=None):
         si, p, L = self.chunks[c]
         s = self.segments[si]
         b = self.buf[slot]
         spec = _lib.PbgSynthSpec(self.seed, s.contig, self.mean_depth, p, L)
+        st = (stream or self.gen_stream).cuda_stream
         self.ctx.check(self.ctx.lib.pbg_synth_pileup(self.ctx.h, C.byref(spec), b["ref"].data_ptr(), b["k"].data_ptr(),
                                                      b["rmsq"].data_ptr(), b["block_off"].data_ptr(),
-                                                     b["keys"].data_ptr(), self.keys_cap, None,
-                                                     self.gen_stream.cuda_stream), "pbg_synth_pileup")
+                                                     b["keys"].data_ptr(), self.keys_cap, None, st), "pbg_synth_pileup")
 
     def _call(self, c: int, slot: int):
         si, p, L = self.chunks[c]
@@ -185,7 +200,16 @@ class GenomePass:
                        "pbg_call_sites")
 
     def call_all(self):
-        """Every chunk: generate (producer stream) -> call (call stream), double-buffered."""
+        """Every chunk: generate (producer stream) -> call (call stream), double-buffered; or,
+        serial, generate -> call on the call stream."""
+        if self.serial:
+            for c in range(len(self.chunks)):
+                self._generate(c, 0, self.call_stream)
+                self._call(c, 0)
+                nb = (self.chunks[c][2] + SITE_BLOCK - 1) // SITE_BLOCK
+                with torch.cuda.stream(self.call_stream):
+                    self.key_total += self.buf[0]["block_off"][nb:nb + 1]
+            return
         for c in range(len(self.chunks)):
             slot = c & 1
             with torch.cuda.stream(self.gen_stream):

@@ -116,7 +116,10 @@ SCENARIOS = {
                               ["sfs", "-w", "2", "REGION=chr1:777-14777"], ["ld", "-w", "1", "REGION=chr1:5001-11000"],
                               ["nucdiv", "REGION=chr1:5000"], ["nucdiv", "-w", "3", "REGION=chr1:3001-12000"],
                               ["snp", "REGION=chr1:4001-4800"], ["nucdiv", "-w", "1", "-m", "0", "-q", "0"],
-                              ["sfs", "-w", "1", "-m", "0", "-q", "0"], ["snp", "-m", "0", "-q", "0", "REGION=chr1:6500-8500"]],
+                              ["sfs", "-w", "1", "-m", "0", "-q", "0"], ["snp", "-m", "0", "-q", "0", "REGION=chr1:6500-8500"],
+                              # -x 0 keeps no read (qfilter fails unless -m 0 -q 0); -x beyond 65535
+                              ["nucdiv", "-w", "1", "-x", "0"], ["nucdiv", "-w", "1", "-x", "0", "-m", "0", "-q", "0"],
+                              ["sfs", "-w", "2", "-x", "70000"]],
                         gap=[(7000, 7600)]),
     # G13: snp output formats -o 1 (SweepFinder) / -o 2 (ms), windows, outgroup flip, 3 populations
     "g13_snpformats": dict(seed=1313, L=12000, samples=_samples(12, ["p1", "p2", "p3"]), step=10, mu=0.03,

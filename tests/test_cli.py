@@ -88,6 +88,53 @@ def test_cli_popbam_world_reports_rank_errors(tmp_path):
     assert r.stderr.decode().count("Bad genome coordinates: chrX:1-100") == 1
 
 
+def test_cli_popbam_world_reports_gpu_side_errors():
+    """A rank failing after the options are parsed, on the library side (pbg_create refuses
+    device 99: PbgError, not a PopbamError) still reaches the gather: status 1, one message,
+    no hang (only PopbamError used to be caught)."""
+    import subprocess
+    import sys
+    d = fixtures.load_case("g01_base")["dir"]
+    env = dict(os.environ, POPBAM_WORLD="2", POPBAM_DEVICE="99")
+    r = subprocess.run([sys.executable, "-m", "popbam_amd.cli", "nucdiv", "-f", os.path.join(d, "ref.fa"), "-w", "1",
+                        os.path.join(d, "in.bam"), "chr1"], env=env, capture_output=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 1 and r.stdout == b"", r.stderr.decode()
+    err = r.stderr.decode()
+    assert err.count("popbam runtime error:") == 1 and "PbgError" in err
+
+
+def test_negative_max_depth_is_refused(capsys):
+    d = fixtures.load_case("g01_base")["dir"]
+    rc, out, err = _main(["nucdiv", "-f", os.path.join(d, "ref.fa"), "-x", "-5", os.path.join(d, "in.bam"), "chr1"],
+                         capsys)
+    assert rc == 1 and out == "" and "-x -5 must not be negative" in err
+
+
+BLOCK_CASES = [c for c in CASES if "-w" in fixtures.load_case(c[0])["meta"]["cases"][c[1]]["args"]
+               and c[0] in ("g01_base", "g12_regions", "g13_snpformats", "g11_eleven")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,idx", BLOCK_CASES, ids=[f"{n}-{i:02d}" for n, i in BLOCK_CASES])
+def test_cli_block_streaming_matches_reference(gpu_lib, name, idx, monkeypatch):
+    """POPBAM_BLOCK_SITES of two windows: the region runs as many blocks (the next block's
+    pileup read while the GPU runs this one, snp -o 2's header only in the first block) and
+    the concatenated text is still the reference's."""
+    cs = fixtures.load_case(name)["meta"]["cases"][idx]
+    a = cs["args"]
+    w = int(a[a.index("-w") + 1]) * 1000
+    monkeypatch.setenv("POPBAM_BLOCK_SITES", str(2 * w))
+    argv = _argv(name, cs)
+    ours = cli.run(argv[0], argv[1:])
+    gold = fixtures.golden_text(name, cs["stdout"])
+    oob = None
+    if a[0] == "snp":
+        oob = harness.snp_oob_cells(harness.oracle_run(harness.Setup(name, a, cs["region"])))
+    ok, diff = harness.same_output(a, gold, ours, oob)
+    assert ok, f"{argv}\n gold: {diff[0]}\n ours: {diff[1]}"
+
+
 def _main(argv, capsys):
     rc = cli.main(argv)
     out = capsys.readouterr()

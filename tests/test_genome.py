@@ -114,3 +114,61 @@ def test_overlapping_pass_matches_one_batch(gpu_lib):
         assert np.array_equal(x.view(np.uint8), hp.out.t[f].cpu().numpy().view(np.uint8)), f
     assert (hp.out.t["segsites"].cpu().numpy() > 0).mean() > 0.5
     ctx.close()
+
+
+def _rank_plan_worker(rank, world, port, results):
+    """One gloo rank: its bench_genome split (genome.rank_plan) for configs[3] and configs[4],
+    gathered on rank 0 over gloo (the only collective the bench uses, on the host)."""
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        mine = {}
+        for config, lengths, win, step in ((3, [125_000_000] * 24, 10_000, 0), (4, [200_000_000], 1000, 500)):
+            segs, stats = genome.rank_plan(config, lengths, world, rank, win, step)
+            mine[config] = ([(s.contig, s.beg, s.end, s.step, s.win_lo, s.win_hi) for s in segs], stats)
+        got = [None] * world
+        dist.all_gather_object(got, mine)
+        if rank == 0:
+            results.update({r: got[r] for r in range(world)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world8_rank_split_covers_genome():
+    """bench.py's N = 8 split, run as 8 gloo processes: configs[3] windows land on exactly one
+    rank each with per-rank loads within one window of the mean (24 equal contigs over 8 ranks:
+    3 whole contigs each); configs[4]'s overlapping-window blocks tile the window list in rank
+    order, each with its win - step halo."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    world = 8
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_rank_plan_worker, args=(world, port, results), nprocs=world, join=True)
+    res = [results[r] for r in range(world)]
+    lengths, win = [125_000_000] * 24, 10_000
+    seen = set()
+    loads = []
+    for r in range(world):
+        segs, stats = res[r][3]
+        assert stats == res[0][3][1]
+        loads.append(sum(e - b for _, b, e, *_ in segs))
+        for ci, b, e, *_ in segs:
+            for w in genome.contig_windows(e, win, b, e):
+                assert (ci, w) not in seen
+                seen.add((ci, w))
+    assert seen == {(ci, w) for ci, L in enumerate(lengths) for w in genome.contig_windows(L, win)}
+    assert max(loads) - min(loads) <= win and sum(loads) == sum(lengths)
+    # configs[4]: window k*step .. k*step + win, contiguous blocks in rank order
+    step, win4, L4 = 500, 1000, 200_000_000
+    nwin = (L4 - win4) // step + 1
+    k = 0
+    for r in range(world):
+        (seg,), _ = res[r][4]
+        ci, b, e, st, lo, hi = seg
+        assert st == step and lo == k * step and b == lo and e == (hi // step - 1) * step + win4
+        k = hi // step
+    assert k == nwin

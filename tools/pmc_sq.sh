@@ -1,13 +1,17 @@
 #!/bin/bash
-# SQ/TA counter passes over a short bench run (one --pmc pass each, separate processes).
+# SQ (and TCC) counter passes over a short configs[2] bench run, one --pmc pass per process,
+# each under its own kill timeout; then the per-kernel summary (tools/pmc_summary.py).
+#   PASSES: ';'-separated counter sets (default: instruction mix + wave states)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out/pmc; export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---sites 10000000 --steps 2 --warmup 0 --cpu-sample 0}
-timeout -k 10 120 rocprofv3 --list-avail > gpurun_out/pmc/list_avail.txt 2>&1
+ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --cpu-sample 0}
+DEF="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU;SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT;FETCH_SIZE;WRITE_SIZE"
+IFS=';' read -ra SETS <<< "${PASSES:-$DEF}"
 i=0
-for set in "$@"; do
+for set in "${SETS[@]}"; do
   i=$((i+1))
+  rm -rf "gpurun_out/pmc/p$i"
   timeout -s KILL 120 rocprofv3 --pmc $set -T --output-format csv -d "$R/gpurun_out/pmc/p$i" -o run \
-    -- python3 "$R/bench.py" $ARGS > gpurun_out/pmc/p$i.log 2>&1 || exit $?
+    -- python3 "$R/bench.py" $ARGS > gpurun_out/pmc/p$i.log 2>&1 || { echo "pass $i ($set) failed"; exit 1; }
 done
-exit 0
+python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.txt && cat gpurun_out/pmc/summary.txt
