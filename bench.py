@@ -45,6 +45,11 @@ def parse():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xC0FFEE02)
     ap.add_argument("--cpu-sample", type=int, default=60_000, help="positions for the CPU port baseline (0 = skip all)")
     ap.add_argument("--ref-sample", type=int, default=200_000, help="positions for the reference-binary baseline")
+    ap.add_argument("--e2e-chunk", type=int, default=4_000_000,
+                    help="config 2: positions per chunk of the measured host-input pass (0 = skip)")
+    ap.add_argument("--e2e-passes", type=int, default=2)
+    ap.add_argument("--cli-sample", type=int, default=200_000,
+                    help="config 2: positions of the BAM the drop-in CLI is timed on (0 = skip)")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
                     help="BASELINE.json configs[i]: 2 = 50 Msites x 12 samples (the metric's config), "
                          "3 = whole genome 24 contigs x 125 Mbp x 24 samples, nucdiv+sfs+ld+diverge, "
@@ -190,6 +195,82 @@ def pcie_rate(torch, batch_bytes: int, step_s: float, sites: int) -> dict:
     return {"h2d_GBps": round(gbps, 2), "batch_bytes": batch_bytes, "copy_ms": round(copy_s * 1e3, 2),
             "Msites_per_s_serial": round(sites / (copy_s + step_s) / 1e6, 2),
             "Msites_per_s_overlapped": round(sites / max(copy_s, step_s) / 1e6, 2)}
+
+
+def end_to_end(args, torch, hp, stream) -> dict:
+    """Measured host-input rate: the same contig handed over in
+    pinned HOST memory, streamed host -> device in chunks of whole windows on a copy stream
+    while the previous chunk is called and its windows computed (workload.HostStream, double
+    buffered); wall time of whole passes.  The pass's rows and window outputs are checked
+    against the HBM-resident step's."""
+    want_rows = hp.rows.clone()
+    want = {k: hp.out.t[k].clone() for k in ("num_sites", "segsites", "pi", "td", "ld_val")}
+    host = hp.to_host()
+    hs = hp.host_stream(host, args.e2e_chunk, args.window)
+    hp.rows.zero_()
+    for k in want:
+        hp.out.t[k].zero_()
+    hs.run(stream)   # warmup pass (plans, slots)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(hp.rows, want_rows)) and all(bool(torch.equal(hp.out.t[k], v)) for k, v in want.items())
+    passes = max(1, args.e2e_passes)
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        hs.run(stream)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / passes
+    del host
+    return {"Msites_per_s": round(args.sites / dt / 1e6, 2), "ms_per_pass": round(dt * 1e3, 2),
+            "h2d_bytes_per_pass": hs.h2d_bytes, "h2d_GBps_effective": round(hs.h2d_bytes / dt / 1e9, 2),
+            "chunk_sites": hs.chunk, "chunks": len(hs.chunks), "passes": passes,
+            "matches_resident": same,
+            "how": "pinned host batch (SURVEY 8(d) layout) -> H2D on a copy stream into two device slots, "
+                   "pbg_call_sites + pbg_window_stats per chunk on the compute stream; wall time per pass"}
+
+
+def cli_rate(args) -> dict:
+    """The drop-in command line on a real BAM: `bin/popbam nucdiv|sfs|ld -f ref.fa -w 10 in.bam
+    chr1` over the same BAM the reference baseline reads (tests/ref_baseline.py, the first
+    --cli-sample positions), each as a fresh process (wall, including interpreter and GPU
+    start-up) and in-process (popbam_amd.cli.run: BAM decode + pileup + key batch on the host
+    feeder's threads, then the GPU), stdout compared with POPBAM's own."""
+    import subprocess
+
+    import ref_baseline
+    from popbam_amd import cli
+    L, n = args.cli_sample, args.samples
+    d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_v3_{args.seed:x}_{L}_{n}", args.seed, L, n)
+    win_kb = str(args.window // 1000)
+    threads = int(os.environ.get("POPBAM_FEED_THREADS", min(8, os.cpu_count() or 1)))
+    res = {"sites": L, "samples": n, "feeder_threads": threads, "commands": {}}
+    tot_proc = tot_in = 0.0
+    same = True
+    for c in ("nucdiv", "sfs", "ld"):
+        argv = [c, "-f", "ref.fa", "-w", win_kb, "in.bam", "chr1"]
+        t0 = time.perf_counter()
+        p = subprocess.run([sys.executable, os.path.join(REPO, "bin", "popbam"), *argv], cwd=d, capture_output=True)
+        t_proc = time.perf_counter() - t0
+        cwd = os.getcwd()
+        os.chdir(d)
+        try:
+            t0 = time.perf_counter()
+            text = cli.run(c, argv[1:])
+            t_in = time.perf_counter() - t0
+        finally:
+            os.chdir(cwd)
+        ok = p.returncode == 0 and p.stdout.decode() == text
+        if ref_baseline.available():
+            r = subprocess.run([ref_baseline.REF_BIN, *argv], cwd=d, capture_output=True)
+            ok = ok and r.stdout.decode() == text
+        same &= ok
+        res["commands"][c] = {"process_s": round(t_proc, 3), "in_process_s": round(t_in, 3)}
+        tot_proc += t_proc
+        tot_in += t_in
+    res.update({"Msites_per_s_process": round(L / tot_proc / 1e6, 4), "Msites_per_s_in_process": round(L / tot_in / 1e6, 4),
+                "identical_to_reference": same,
+                "note": "3 commands summed, as the CPU baseline; a fresh process pays Python + torch import and "
+                        "context creation; in-process is the feeder + GPU path alone"})
+    return res
 
 
 def max_over_ranks(dist, x: float) -> float:
@@ -436,6 +517,10 @@ def main():
         }
         if world == 1:
             out["pcie_inclusive"] = pcie_rate(torch, layout_bytes - args.sites * n, elapsed / args.steps, args.sites)
+            if args.e2e_chunk > 0 and args.cpu_sample > 0:   # --cpu-sample 0 (profiling runs) skips the extras
+                out["end_to_end"] = end_to_end(args, torch, hp, stream)
+            if args.cli_sample > 0 and args.cpu_sample > 0:
+                out["cli"] = cli_rate(args)
         if world == 1 and args.cpu_sample > 0:
             out["cpu_baseline"] = cpu_baseline(args)
         else:
