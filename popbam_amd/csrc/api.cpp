@@ -27,6 +27,7 @@ struct pbg_ctx {
     double *d_fk = nullptr, *d_beta = nullptr, *d_lhet = nullptr, *d_sfs = nullptr, *d_r2 = nullptr;
     double *d_fbeta = nullptr;
     double *d_lb = nullptr;
+    double *d_oe = nullptr;
     int *d_err = nullptr;
     std::string err;
     // per-pileup LDS staging capacity (keyed by block_off pointer and size), so repeated
@@ -224,6 +225,12 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
             }
         }
         if ((e = upload(&c->d_lb, lb)) != hipSuccess) return bad(e, "upload lb");
+        std::vector<double> oe(pbg::kOeSize, 0.0);
+        for (int q = 4; q < 64; ++q)
+            for (int d = 0; d <= 16; ++d) oe[(q - 4) * 17 + d] = beta[q << 16 | d << 8];
+        for (int nn = 0; nn <= 16; ++nn)
+            for (int kk = 0; kk <= 16; ++kk) oe[60 * 17 + nn * 17 + kk] = lhet[nn << 8 | kk];
+        if ((e = upload(&c->d_oe, oe)) != hipSuccess) return bad(e, "upload one-error tables");
     }
     // Tajima constants are indexed by population size and built for n = sm->n (pop_sfs.cpp:53-56)
     std::vector<double> a1, a2, e1, e2;
@@ -250,6 +257,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     c->dt.lhet = c->d_lhet;
     c->dt.fbeta = c->d_fbeta;
     c->dt.lb = c->d_lb;
+    c->dt.oe = c->d_oe;
     c->dt.a1 = c->d_sfs;
     c->dt.a2 = c->d_sfs + L;
     c->dt.e1 = c->d_sfs + 2 * L;
@@ -269,7 +277,7 @@ void pbg_destroy(pbg_ctx *c) {
         (void)hipEventDestroy(c->ev_deep);
     }
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
-                    (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, (void *)c->d_zns,
+                    (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_oe, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, (void *)c->d_zns,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
                     (void *)c->deep.blk_cnt, (void *)c->deep.raw,
                     (void *)c->d_segcnt, (void *)c->d_synth})

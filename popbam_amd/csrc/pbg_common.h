@@ -52,12 +52,17 @@ struct DevTables {
     // (q 4..63, d 3..16): with m0 / m1 reference-base keys per strand, all of quality >= q,
     // errmod_cal's bsum of that base is >= (fk_prefix[m0] + fk_prefix[m1]) * bmin[q][d]
     const double *lb;     // [17 + 60 * 17]
+    // one-error tables in compact form (the scan kernel reads them through L1 / L2):
+    // [0, 60 * 17) beta[q<<16|d<<8|0] at (q - 4) * 17 + d; then [60 * 17, 60 * 17 + 17 * 17)
+    // lhet[n<<8|k] at 60 * 17 + n * 17 + k (n, k <= 16)
+    const double *oe;     // [60 * 17 + 17 * 17]
     const double *a1, *a2, *e1, *e2;          // Tajima/Fay-Wu constants (pop_sfs.cpp:511-571)
     const double *r2;     // concatenated per-population r^2 tables, see r2_off
     int32_t r2_off[PBG_MAX_POPS];             // offset of population p's (n_p+1)^3 table
 };
 
 constexpr int kLbSize = 17 + 60 * 17;
+constexpr int kOeSize = 60 * 17 + 17 * 17;
 constexpr int kFbetaN = 17;   // n in [0, 16]
 __host__ __device__ inline uint32_t fbeta_index(uint32_t q, uint32_t n, uint32_t c, uint32_t w) {
     return ((q * kFbetaN + n) << 8) | (c << 4) | w;
@@ -219,10 +224,12 @@ struct DeepBufs {
     DeepTask *tasks;    // [task_cap]
     uint8_t *info;      // [n_sites * n]
     uint32_t *count;    // [0] positions, [1] tasks (may exceed task_cap: computed in place),
-                        // [2] rows-only pipeline: nonzero when a task was marked for the overflow kernel
+                        // [2] rows-only pipeline: blocks listed for the overflow kernel,
+                        // [3] rows-only pipeline: deep tasks appended to `tasks` (dense list)
     uint32_t task_cap;
-    // rows-only pipeline: block b owns tasks[b*blk_cap, (b+1)*blk_cap): tasks with at most 16
-    // reads from the start, deeper ones from the end; blk_cnt[b] = shallow | deep << 16
+    // rows-only pipeline: block b owns raw entries [b*blk_cap, (b+1)*blk_cap) for the tasks with
+    // at most 16 reads the scan could not settle (blk_cnt[b] of them); tasks with more reads
+    // are a dense list tasks[0, count[3]) (at most task_cap)
     uint32_t *blk_cnt;
     uint32_t blk_cap;
     uint4 *raw;         // [nblk*blk_cap*2]: the 16 keys of front (<= 16 keys) entries (32 B, the
@@ -233,10 +240,6 @@ struct DeepBufs {
 #define PBG_QGROUP 16
 #endif
 constexpr int kQueueGroup = PBG_QGROUP;   // blocks per wave in the queue kernels
-#ifndef PBG_DEEP_GROUP
-#define PBG_DEEP_GROUP 64
-#endif
-constexpr int kDeepGroup = PBG_DEEP_GROUP;   // blocks per wave in call_deepq_kernel (few deep tasks)
 
 // A device pileup batch as the kernels see it (pbg_pileup with the k width resolved).
 struct Batch {
