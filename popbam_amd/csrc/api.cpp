@@ -279,7 +279,7 @@ void pbg_destroy(pbg_ctx *c) {
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
                     (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_oe, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, (void *)c->d_zns,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
-                    (void *)c->deep.blk_cnt, (void *)c->deep.raw,
+                    (void *)c->deep.blk_cnt, (void *)c->deep.raw, (void *)c->deep.pend,
                     (void *)c->d_segcnt, (void *)c->d_synth})
         if (p) (void)hipFree(p);
     for (auto &t : c->tmpl) (void)hipFree(t.second);
@@ -322,10 +322,11 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
     // consensus-word pipeline's deep queue shares the task array
     if (c->deep_sites_cap < pl->n_sites || c->deep_info_cap < (size_t)pl->n_sites * c->dp.n) {
         for (void *p : {(void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.blk_cnt,
-                        (void *)c->deep.raw})
+                        (void *)c->deep.raw, (void *)c->deep.pend})
             if (p) HIPCHK(c, hipFree(p));
         c->deep.blk_cnt = nullptr;
         c->deep.raw = nullptr;
+        c->deep.pend = nullptr;
         c->deep.sites = nullptr;
         c->deep.tasks = nullptr;
         c->deep.info = nullptr;
@@ -335,11 +336,12 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         const size_t tcap = std::max<size_t>((size_t)nblk * blk_cap, std::min<size_t>(ntask / 32 + 65536, 0xFFFFFFFFu));
         HIPCHK(c, hipMalloc((void **)&c->deep.sites, (size_t)pl->n_sites * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc((void **)&c->deep.tasks, tcap * sizeof(pbg::DeepTask)));
-        HIPCHK(c, hipMalloc((void **)&c->deep.info, ntask));
+        HIPCHK(c, hipMalloc((void **)&c->deep.info, ntask + 64));   // + slack: the scan's fold reads whole dwords
+        HIPCHK(c, hipMalloc((void **)&c->deep.pend, (size_t)nblk * sizeof(uint64_t)));
         c->deep.task_cap = (uint32_t)std::min<size_t>(tcap, 0xFFFFFFFFu);
         c->deep.blk_cap = blk_cap;
         HIPCHK(c, hipMalloc((void **)&c->deep.blk_cnt, (size_t)nblk * sizeof(uint32_t)));
-        HIPCHK(c, hipMalloc((void **)&c->deep.raw, (size_t)nblk * blk_cap * 2 * sizeof(uint4)));
+        HIPCHK(c, hipMalloc((void **)&c->deep.raw, (size_t)nblk * blk_cap * sizeof(uint4)));
         c->deep_sites_cap = pl->n_sites;
         c->deep_info_cap = ntask;
     }

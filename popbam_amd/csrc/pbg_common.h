@@ -227,14 +227,14 @@ struct DeepBufs {
                         // [2] rows-only pipeline: blocks listed for the overflow kernel,
                         // [3] rows-only pipeline: deep tasks appended to `tasks` (dense list)
     uint32_t task_cap;
-    // rows-only pipeline: block b owns raw entries [b*blk_cap, (b+1)*blk_cap) for the tasks with
-    // at most 16 reads the scan could not settle (blk_cnt[b] of them); tasks with more reads
+    // rows-only pipeline: block b owns queue records raw[b*blk_cap, (b+1)*blk_cap) for the tasks
+    // with at most 16 reads the scan could not settle (blk_cnt[b] of them); tasks with more reads
     // are a dense list tasks[0, count[3]) (at most task_cap)
     uint32_t *blk_cnt;
     uint32_t blk_cap;
-    uint4 *raw;         // [nblk*blk_cap*2]: the 16 keys of front (<= 16 keys) entries (32 B, the
-                        // entry header in key bits 11-15), copied by the scan kernel from its LDS
-                        // staging so the queue kernel loads them coalesced
+    uint64_t *pend;     // rows-only pipeline: per block, the positions whose row waits for a queued task
+    uint4 *raw;         // [nblk*blk_cap] queue records {site, sample | k << 8 | tried << 31, first key
+                        // (u64)}: call_slow_kernel re-reads the task's keys
 };
 #ifndef PBG_QGROUP
 #define PBG_QGROUP 16
