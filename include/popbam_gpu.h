@@ -90,7 +90,10 @@ typedef struct {
  *                 it from k[] when NULL)
  *   keys[]        one u16 per kept read, (position, sample, pileup order) major:
  *                 qq<<5 | strand<<4 | base (popbam.cpp:284), qq = clamp(min(baseQ, mapQ), 4, 63)
- * Device batches: keys[] must be 16-byte aligned (any hipMalloc / torch allocation is).   */
+ * Device batches: keys[] must be 16-byte aligned (any hipMalloc / torch allocation is).
+ * block_off[0] need not be 0: the kernels read only the 16-byte chunks of keys[] that hold
+ * keys [block_off[0], block_off[last]), so a caller may pass keys shifted back by a
+ * multiple of 8 keys to address a buffer that holds only that range.                     */
 typedef struct {
     uint32_t        n_sites;
     int32_t         pos0;

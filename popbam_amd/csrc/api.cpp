@@ -527,7 +527,7 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     A.ld_ns = c->d_segcnt + n_win + (size_t)n_win * np;
     A.lds = pbg::stats_lds_layout(n, np, c->dp.sfs_stride, o->stats, 0, (int)mw);
     if (A.lds.bytes > 64 * 1024) return fail(c, PBG_E_ARG, "statistics need more LDS than a workgroup has");
-    HIPCHK(c, pbg::launch_window_stats(c->row_bytes, c->dp, c->dt, rows, n_rows, n_win, A, (hipStream_t)stream));
+    HIPCHK(c, pbg::launch_window_stats(c->row_bytes, c->dp, c->dt, rows, n_rows, n_win, A, (hipStream_t)stream, c->n_cu));
     return PBG_OK;
 }
 

@@ -269,6 +269,6 @@ hipError_t launch_synth(const DevParams &P, uint64_t seed, int contig, int mean_
 hipError_t launch_synth_tmpl(uint64_t seed, uint16_t *tmpl, hipStream_t stream);
 size_t synth_scratch_words(uint32_t n_sites);
 hipError_t launch_window_stats(int row_bytes, const DevParams &P, const DevTables &T, const void *rows,
-                               uint32_t n_rows, uint32_t n_win, const StatsArgs &A, hipStream_t stream);
+                               uint32_t n_rows, uint32_t n_win, const StatsArgs &A, hipStream_t stream, int n_cu);
 
 }  // namespace pbg

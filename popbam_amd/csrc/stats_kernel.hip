@@ -746,118 +746,197 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
     if (O.ld_val) O.ld_val[(size_t)w * np + i] = x86nan(val);
 }
 
-// list entries of a chain staged in LDS (longer lists: read from the pool), and the slot
-// stride: +16 B staggers the slots' LDS banks
-template <class M>
-constexpr int zns_stage() { return sizeof(M) == 8 ? 256 : 128; }
-template <class M>
-constexpr int zns_stride() { return zns_stage<M>() + (sizeof(M) == 8 ? 2 : 1); }
-// ZnS sums, 16 lanes per chain: each 16-lane row of a wave owns one (window, population)
-// chain; per step its lanes compute the r^2 of the next 16 pairs of the current row a (lanes
-// past the row's end give +0.0) and the row's first lane adds the 16 values in pair order
-// (broadcast LDS reads), so the chain is the reference's exact sequence of additions with
-// 16-wide r^2 work.  Four chains per wave, 16 per workgroup.
-constexpr int kZnsRowUnroll = 1;   // steps per pipelined round (1: 0.37 ms of statistics at configs[2]; 2: 0.38; 4: 0.40)
-template <class M>
-__global__ __launch_bounds__(256) void window_zns_row_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A,
-                                                             int r2_lds) {
-    constexpr int kStage = zns_stage<M>(), kStride = zns_stride<M>();
-    extern __shared__ __align__(16) double s_dyn[];
-    // a step's r^2 per chain; +2 doubles per chain so the four rows of a wave read different banks
-    __shared__ __align__(16) double s_val[16][2 * (16 * kZnsRowUnroll + 2)];   // two halves (pipelined rounds)
-    double *s_r2t = s_dyn;                                                      // [r2_lds]
-    M *s_t = reinterpret_cast<M *>(s_dyn + r2_lds);                            // [16][kStride] masks
-    for (int i = threadIdx.x; i < r2_lds; i += 256) s_r2t[i] = T.r2[i];
-    const int np = P.npops;
-    const int lane = threadIdx.x & 63, g = lane & 15, q = (int)(threadIdx.x >> 4);   // q: chain slot 0..15
-    double *sv = s_val[q];
-    const uint32_t nch = n_win * (uint32_t)np;
-    const uint32_t ch = blockIdx.x * 16 + (uint32_t)q;
-    int V = 0;
-    const M *L = reinterpret_cast<const M *>(A.pool);
-    int np1 = 1, r2o = 0;
-    if (ch < nch) {
-        const uint32_t w = ch / (uint32_t)np;
-        const int i = (int)(ch - w * (uint32_t)np);
-        V = A.var_count[ch];
-        L = reinterpret_cast<const M *>((A.zstride ? A.zlist : A.pool) + A.zoff[ch]);
-        np1 = P.pop_n[i] + 1;
-        r2o = T.r2_off[i];
+// ZnS (calc_zns, pop_ld.cpp:201-252) as producer / consumer.  The reference's value of a
+// (window, population) chain is one sequential double sum of r^2 over every pair (a, b), a < b,
+// of the population's variable sites, in pair order: V(V-1)/2 dependent additions.  A workgroup
+// owns C consecutive chains and has 64 + 16 C threads.  Wave 0 is the adder: lane c keeps chain
+// c's running double and, per round, adds the chain's next 16 values in pair order from an LDS
+// ring (eight 16-byte reads issued a round ahead, then 16 register adds: the dependent chain
+// never waits on another lane).  Producer group c (16 lanes) walks chain c a row step per round:
+// lane j computes r^2 of pair (a, b0 + j) from the popcounts of the two sites' masks and of their
+// intersection (the host's r^2 table); lanes past the row's end give +0.0, which leaves the sum
+// unchanged, so the adder sees the reference's exact sequence of additions.  Rounds run in
+// phases of kZnsR: while the adder sums phase k - 1 from one half of the ring, the producers
+// fill the other half with phase k; one workgroup barrier per phase.
+//
+// Fast path (every population of at most 32 samples and every list of the workgroup within the
+// LDS list capacity): the lists are staged in LDS as {population-compacted 32-bit mask,
+// popcount * (n_p + 1)} and the r^2 tables sit in LDS with a 0.0 slot past them, so a pair is
+// two LDS reads (the row's entry a broadcast), four VALU and the table read.  Otherwise the raw
+// masks (u64 / two-word) are read from the list buffer in HBM / L2, the table from LDS or HBM.
+constexpr int kZnsMaxC = 60;                 // chains per workgroup (64 + 16 C <= 1024 threads)
+constexpr int kZnsR = 4;                     // rounds per phase
+constexpr int kZnsRingStride = 18;           // doubles per (round, chain): 16 values + 2 pad (LDS banks)
+
+// the sample bits of t inside population mask pm, packed to bit positions 0..pc(pm)-1
+__device__ __forceinline__ uint32_t pext32(uint64_t t, uint64_t pm, uint32_t &k) {
+    uint32_t out = 0;
+    while (pm) {
+        const int p = __builtin_ctzll(pm);
+        out |= (uint32_t)((t >> p) & 1u) << k;
+        ++k;
+        pm &= pm - 1;
     }
-    // the wave's four chains staged in LDS, or all read from the pool (wave-uniform)
-    const bool staged = !__ballot(V > kStage);
-    M *lt = s_t + q * kStride;
-    if (staged)
-        for (int j = g; j < V; j += 16) lt[j] = L[j];
+    return out;
+}
+__device__ __forceinline__ uint32_t compact32(uint64_t t, uint64_t pm) {
+    uint32_t k = 0;
+    return pext32(t, pm, k);
+}
+__device__ __forceinline__ uint32_t compact32(M2 t, M2 pm) {
+    uint32_t k = 0;
+    const uint32_t lo = pext32(t.lo, pm.lo, k);
+    return lo | pext32(t.hi, pm.hi, k);
+}
+// row-step rounds of a chain of V sites: sum over the V - 1 rows of ceil(row length / 16)
+__device__ __forceinline__ long long zns_rounds(int V) {
+    const long long N = V > 1 ? V - 1 : 0, q = N / 16, r = N % 16;
+    return (q + 1) * (8 * q + r);
+}
+
+struct ZnsChain {   // per-chain constants, LDS
+    const void *list;   // the chain's raw masks (M) in the list buffer
+    int32_t V, np1, r2o, ns;
+    int32_t w;
+};
+
+template <class M>
+__global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables T, uint32_t n_win, StatsArgs A,
+                                                          int r2_lds, int C, int cap, int compact) {
+    extern __shared__ __align__(16) double s_dyn[];
+    __shared__ ZnsChain s_ch[kZnsMaxC];
+    __shared__ long long s_rounds;
+    __shared__ int s_fits;
+    const int tid = (int)threadIdx.x, np = P.npops, nthr = (int)blockDim.x;
+    const uint32_t nch = n_win * (uint32_t)np;
+    const uint32_t ch0 = blockIdx.x * (uint32_t)C;
+    // LDS: r^2 tables (+ a 0.0 slot) | ring [2][kZnsR][C][kZnsRingStride] | lists [C][cap] uint2
+    double *s_r2t = s_dyn;
+    const int r2_slots = r2_lds ? ((r2_lds + 2) & ~1) : 0;
+    double *s_ring = s_dyn + r2_slots;
+    uint2 *s_lst = reinterpret_cast<uint2 *>(s_ring + 2 * kZnsR * C * kZnsRingStride);
+    const size_t rstride = (size_t)C * kZnsRingStride;   // doubles per round
+    if (tid == 0) {
+        s_rounds = 0;
+        s_fits = compact;
+    }
+    for (int i = tid; i < r2_lds; i += nthr) s_r2t[i] = T.r2[i];
+    if (tid == 0 && r2_lds) s_r2t[r2_lds] = 0.0;
     __syncthreads();
-    // Software-pipelined rounds: round i's values are read from one half of the chain's LDS
-    // buffer while round i+1's r^2 values are produced into registers (their list / table loads
-    // in flight during the reads, their VALU free to interleave with round i's dependent adds --
-    // one basic block, no exec-mask branches), then stored to the other half.  Row-step order
-    // (b0 .. b0+15 of row a per step; lanes past the row's end give +0.0).
-    auto run_pipe = [&](const M *lst, const double *r2p) -> double {
-        constexpr int U = kZnsRowUnroll, kHalf = 16 * U + 2;
-        const int vm1 = V > 0 ? V - 1 : 0;
-        int a = 0, b0 = 1;
-        double r[U];
-        auto produce = [&]() {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int b = b0 + g;
-                const bool ok = (a < V - 1) & (b < V);
-                const M ta = lst[min(a, vm1)], tb = lst[min(b, vm1)];
-                const double rv = r2p[((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
-                r[u] = ok ? rv : 0.0;
-                b0 += 16;
-                const bool nxt = (b0 >= V) & (a < V - 1);
-                a += nxt ? 1 : 0;
-                b0 = nxt ? a + 1 : b0;
+    if (tid < C) {
+        const uint32_t ch = ch0 + (uint32_t)tid;
+        ZnsChain z{nullptr, 0, 1, 0, 0, 0};
+        if (ch < nch) {
+            const uint32_t w = ch / (uint32_t)np;
+            const int i = (int)(ch - w * (uint32_t)np);
+            z.list = (A.zstride ? A.zlist : A.pool) + A.zoff[ch];
+            z.V = A.var_count[ch];
+            z.np1 = P.pop_n[i] + 1;
+            z.r2o = T.r2_off[i];
+            z.ns = A.ld_ns[ch];
+            z.w = (int)w;
+        }
+        s_ch[tid] = z;
+        atomicMax(reinterpret_cast<unsigned long long *>(&s_rounds), (unsigned long long)zns_rounds(z.V));
+        if (z.V > cap) atomicAnd(&s_fits, 0);
+    }
+    __syncthreads();
+    const long long nphase = (s_rounds + kZnsR - 1) / kZnsR;
+    const bool fast = s_fits != 0 && r2_lds != 0;   // workgroup-uniform
+    if (fast) {   // stage the lists compacted: wave v takes chains v, v + (waves), ...
+        const int wv = tid >> 6, lane = tid & 63, nwv = nthr >> 6;
+        for (int c = wv; c < C; c += nwv) {
+            const ZnsChain z = s_ch[c];
+            const int i = (int)((ch0 + (uint32_t)c) % (uint32_t)np);
+            const M pm = pop_mask<M>(P, i);
+            const M *L = reinterpret_cast<const M *>(z.list);
+            for (int b = lane; b < z.V; b += 64) {
+                const uint32_t m = compact32(L[b], pm);
+                s_lst[c * cap + b] = make_uint2(m, (uint32_t)__popc(m) * (uint32_t)z.np1);
             }
-        };
-        auto put = [&](int c) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) sv[c * kHalf + 16 * u + g] = r[u];
-        };
-        auto sync = [&]() {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        };
+        }
+    }
+    __syncthreads();   // the staged lists
+    if (tid < 64) {
+        // ---- the adder: lane c sums chain c's values in pair order
         double acc = 0.0;
-        bool live = __ballot(a < V - 1) != 0;   // wave-uniform: round 0 has pairs
-        produce();
-        put(0);
-        sync();
-        int c = 0;
-        while (live) {
-            const double2 *sv2 = reinterpret_cast<const double2 *>(sv + c * kHalf);
-            double2 v[8 * U];
+        for (long long k = 0; k <= nphase; ++k) {   // phase k: sum phase k - 1 (the producers write phase k)
+            if (k >= 1 && tid < C) {
+                const double2 *rg = reinterpret_cast<const double2 *>(s_ring + (size_t)((k - 1) & 1) * kZnsR * rstride +
+                                                                      (size_t)tid * kZnsRingStride);
+                double2 v[8];
 #pragma unroll
-            for (int x = 0; x < 8 * U; ++x) v[x] = sv2[x];
-            live = __ballot(a < V - 1) != 0;   // the next round has pairs
-            produce();
+                for (int x = 0; x < 8; ++x) v[x] = rg[x];
 #pragma unroll
-            for (int x = 0; x < 8 * U; ++x) {   // pair order: step u, lane 0..15
-                acc += v[x].x;
-                acc += v[x].y;
+                for (int r = 0; r < kZnsR; ++r) {   // the next round's values are read before this round's adds
+                    double2 nv[8];
+                    if (r + 1 < kZnsR) {
+#pragma unroll
+                        for (int x = 0; x < 8; ++x) nv[x] = rg[(size_t)(r + 1) * (rstride / 2) + x];
+                    }
+#pragma unroll
+                    for (int x = 0; x < 8; ++x) {
+                        acc += v[x].x;
+                        acc += v[x].y;
+                    }
+                    if (r + 1 < kZnsR) {
+#pragma unroll
+                        for (int x = 0; x < 8; ++x) v[x] = nv[x];
+                    }
+                }
             }
-            put(c ^ 1);
-            sync();
-            c ^= 1;
+            __syncthreads();
         }
-        return acc;
-    };
-    double acc;
-    if (staged) acc = r2_lds ? run_pipe(lt, s_r2t + r2o) : run_pipe(lt, T.r2 + r2o);
-    else acc = r2_lds ? run_pipe(L, s_r2t + r2o) : run_pipe(L, T.r2 + r2o);
-    if (g == 0 && ch < nch) {
-        const uint32_t w = ch / (uint32_t)np;
-        double val = 0.0;
-        if (A.seg_count[w] >= 1) {
-            const int ns = A.ld_ns[ch];
-            val = acc * (2.0 / (ns * (ns - 1)));
+        if (tid < C && ch0 + (uint32_t)tid < nch) {
+            const ZnsChain z = s_ch[tid];
+            double val = 0.0;
+            if (A.seg_count[z.w] >= 1) val = acc * (2.0 / (z.ns * (z.ns - 1)));
+            if (A.out.ld_val) A.out.ld_val[ch0 + (uint32_t)tid] = x86nan(val);
         }
-        if (A.out.ld_val) A.out.ld_val[ch] = x86nan(val);
+        return;
+    }
+    // ---- the producers: group c = (tid - 64) / 16 walks chain c, lane j takes pair (a, b0 + j)
+    const int p = tid - 64, j = p & 15, c = p >> 4;
+    const ZnsChain z = s_ch[c];
+    const int V = z.V, V1 = z.V - 1, np1 = z.np1, r2o = z.r2o;
+    int a = 0, b0 = 1;
+    const uint2 *lst = s_lst + c * cap;
+    const M *L = reinterpret_cast<const M *>(z.list);
+    const double *tab = r2_lds ? s_r2t : T.r2;
+    for (long long k = 0; k <= nphase; ++k) {
+        if (k < nphase) {
+            double *out = s_ring + (size_t)(k & 1) * kZnsR * rstride + (size_t)c * kZnsRingStride + j;
+            if (fast) {
+#pragma unroll
+                for (int r = 0; r < kZnsR; ++r) {
+                    const int b = b0 + j;
+                    const bool ok = (a < V1) & (b < V);
+                    const uint2 ea = lst[ok ? a : 0], eb = lst[ok ? b : 0];
+                    const int idx = ok ? r2o + (int)(ea.y * (uint32_t)np1 + eb.y) + __popc(ea.x & eb.x) : r2_lds;
+                    out[(size_t)r * rstride] = s_r2t[idx];
+                    b0 += 16;
+                    const bool nxt = b0 >= V;
+                    a += nxt ? 1 : 0;
+                    b0 = nxt ? a + 1 : b0;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < kZnsR; ++r) {
+                    const int b = b0 + j;
+                    double v = 0.0;
+                    if ((a < V1) & (b < V)) {
+                        const M ta = L[a], tb = L[b];
+                        v = tab[r2o + ((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
+                    }
+                    out[(size_t)r * rstride] = v;
+                    b0 += 16;
+                    const bool nxt = b0 >= V;
+                    a += nxt ? 1 : 0;
+                    b0 = nxt ? a + 1 : b0;
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -867,7 +946,7 @@ template __global__ void window_stats_kernel<8>(DevParams, DevTables, const void
 template __global__ void window_stats_kernel<16>(DevParams, DevTables, const void *, uint32_t, uint32_t, StatsArgs);
 
 hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, const void *rows, uint32_t n_rows,
-                               uint32_t n_win, const StatsArgs &A, hipStream_t stream) {
+                               uint32_t n_win, const StatsArgs &A, hipStream_t stream, int n_cu) {
     if (n_win == 0) return hipSuccess;
     const dim3 g(n_win), b(64);
     const size_t lds = A.lds.bytes;
@@ -878,17 +957,26 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
         default: hipLaunchKernelGGL(window_stats_kernel<16>, g, b, lds, stream, P, T, rows, n_rows, n_win, A); break;
     }
     if (A.stats & PBG_S_ZNS) {
-        int r2_total = 0;
-        for (int i = 0; i < P.npops; ++i) r2_total += (P.pop_n[i] + 1) * (P.pop_n[i] + 1) * (P.pop_n[i] + 1);
-        const int r2_lds = r2_total <= 4608 ? r2_total : 0;   // <= 36 KB of LDS per wave
+        int r2_total = 0, max_pop = 0;
+        for (int i = 0; i < P.npops; ++i) {
+            r2_total += (P.pop_n[i] + 1) * (P.pop_n[i] + 1) * (P.pop_n[i] + 1);
+            max_pop = std::max(max_pop, P.pop_n[i]);
+        }
+        const int r2_lds = r2_total <= 4608 ? r2_total : 0;   // <= 36 KB of LDS
         const uint32_t chains = n_win * (uint32_t)P.npops;
-        const dim3 g((chains + 15) / 16);
+        // C chains per workgroup (64 + 16 C threads): one workgroup per CU when the chains allow it
+        const int C = (int)std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)kZnsMaxC, (chains + n_cu - 1) / std::max(1, n_cu)));
+        const size_t fixed = (size_t)(r2_lds ? ((r2_lds + 2) & ~1) : 0) * 8 + (size_t)2 * kZnsR * C * kZnsRingStride * 8;
+        const size_t budget = 150 * 1024;
+        int cap = budget > fixed ? (int)std::min<size_t>(4096, (budget - fixed) / ((size_t)C * 8)) & ~7 : 0;
+        const int compact = (max_pop <= 32 && r2_lds && cap >= 16) ? 1 : 0;
+        if (!compact) cap = 0;
+        const size_t lds = fixed + (size_t)C * cap * 8;
+        const dim3 g((chains + C - 1) / C), b(64 + 16 * C);
         if (rb == 16)
-            hipLaunchKernelGGL(window_zns_row_kernel<M2>, g, dim3(256), (size_t)r2_lds * 8 + 16 * zns_stride<M2>() * 16,
-                               stream, P, T, n_win, A, r2_lds);
+            hipLaunchKernelGGL(window_zns_kernel<M2>, g, b, lds, stream, P, T, n_win, A, r2_lds, C, cap, compact);
         else
-            hipLaunchKernelGGL(window_zns_row_kernel<uint64_t>, g, dim3(256),
-                               (size_t)r2_lds * 8 + 16 * zns_stride<uint64_t>() * 8, stream, P, T, n_win, A, r2_lds);
+            hipLaunchKernelGGL(window_zns_kernel<uint64_t>, g, b, lds, stream, P, T, n_win, A, r2_lds, C, cap, compact);
     }
     const uint32_t ld = A.stats & (PBG_S_OMEGA | PBG_S_WALL);
     if (ld) {

@@ -385,3 +385,38 @@ def test_pipelined_pieces_equal_one_step(gpu_lib, n, npops, pieces):
         assert torch.equal(one.out.t[k].view(torch.uint8), two.out.t[k].view(torch.uint8)), k
     assert int(one.out.t["segsites"].sum()) > 0
     ctx.close()
+
+
+@pytest.mark.parametrize("n,npops", [(12, 2), (32, 2)])
+def test_host_stream_equals_resident(gpu_lib, n, npops):
+    """The host-input pipeline (workload.HostStream: pinned host batch -> H2D into two device
+    slots per chunk of whole windows, keys pointer shifted back so block_off stays absolute,
+    pbg_call_sites + pbg_window_stats per chunk) writes the same rows and window outputs as one
+    HBM-resident step.  The kernels must read only keys [block_off[0], block_off[last]) of the
+    shifted pointer (include/popbam_gpu.h)."""
+    import torch
+    from popbam_amd import _lib, workload
+    stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS
+    ctx, params = _ctx(n, npops)
+    n_sites = 1_000_000 + 37
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 7 * n)
+    wins = workload.reference_windows(0, n_sites, 10_000)
+    hp = workload.HotPath(ctx, syn, wins, stats)
+    hp.step()
+    ctx.sync_check()
+    want_rows = hp.rows.clone()
+    fields = workload.HotPath.fields_for(stats)
+    want = {k: hp.out.t[k].clone() for k in fields}
+    hs = hp.host_stream(hp.to_host(), 240_000, 10_000)
+    assert len(hs.chunks) >= 4
+    hp.rows.zero_()
+    for k in fields:
+        hp.out.t[k].zero_()
+    for _ in range(2):   # the second pass reuses both slots
+        hs.run(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    ctx.sync_check()
+    assert torch.equal(hp.rows, want_rows)
+    for k in fields:
+        assert torch.equal(hp.out.t[k].view(torch.uint8), want[k].view(torch.uint8)), k
+    ctx.close()
