@@ -60,9 +60,6 @@ struct pbg_ctx {
     std::vector<std::pair<uint64_t, uint16_t *>> tmpl;
     // pbg_run text kept when the caller's buffer was too small (pbg_take_text)
     std::string text;
-    // second stream for the deep-task queue kernel beside the shallow one (pbg_call_sites)
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_scan = nullptr, ev_deep = nullptr;
 };
 
 namespace {
@@ -231,6 +228,37 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
         for (int nn = 0; nn <= 16; ++nn)
             for (int kk = 0; kk <= 16; ++kk) oe[60 * 17 + nn * 17 + kk] = lhet[nn << 8 | kk];
         if ((e = upload(&c->d_oe, oe)) != hipSuccess) return bad(e, "upload one-error tables");
+        std::vector<double> bu(60 * 17, 0.0);   // min over q' >= q, c <= d - 1 of beta[q'][d][c]
+        for (int dd = 1; dd <= 16; ++dd) {
+            double run = 1e300;
+            for (int q = 63; q >= 4; --q) {
+                for (int cc = 0; cc <= dd - 1; ++cc) run = std::min(run, beta[q << 16 | dd << 8 | cc]);
+                bu[(q - 4) * 17 + dd] = run;
+            }
+        }
+        // uniform tasks: het values and the strand-free bound per (d, m class, q); since fk
+        // decreases, fk_prefix[m0] + fk_prefix[m1] >= fk_prefix[m0 + m1], so fk_prefix[d] is a
+        // lower bound of the per-strand sum whatever the strands
+        bool fk_dec = true;   // fk[n] = (1 - depcorr)^n (1 - eta) + eta (pop_utils.cpp:219) decreases
+        for (int w = 1; w < 16; ++w) fk_dec = fk_dec && fk[w] <= fk[w - 1];
+        for (int dd = 1; dd <= 16; ++dd) {
+            float h[2];
+            for (int t = 0; t < 2; ++t) {
+                const float v = (float)(-4.343 * lhet[dd << 8 | (t ? dd : 0)]);
+                h[t] = v < 0.0f ? 0.0f : v;
+                d.uni_het[dd][t] = h[t];
+            }
+            const float hm[3] = {h[0], h[1], std::min(h[0], h[1])};
+            for (int cls = 0; cls < 3; ++cls) {
+                uint64_t bits = 0;
+                for (int q = 4; q < 64; ++q) {
+                    const double lbv = lb[dd] * bu[(q - 4) * 17 + dd];
+                    if (fk_dec && hm[cls] > 0.0f && lbv * (1.0 - 1e-9) > (double)hm[cls] * (1.0 + 1e-6) + 1e-3)
+                        bits |= 1ull << q;
+                }
+                d.uni_ok[dd][cls] = bits;
+            }
+        }
     }
     // Tajima constants are indexed by population size and built for n = sm->n (pop_sfs.cpp:53-56)
     std::vector<double> a1, a2, e1, e2;
@@ -270,12 +298,6 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
 void pbg_destroy(pbg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->aux) {
-        (void)hipStreamSynchronize(c->aux);
-        (void)hipStreamDestroy(c->aux);
-        (void)hipEventDestroy(c->ev_scan);
-        (void)hipEventDestroy(c->ev_deep);
-    }
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
                     (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_oe, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, (void *)c->d_zns,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
@@ -364,14 +386,9 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         ++c->ev_used;
         HIPCHK(c, hipEventRecord(c0, (hipStream_t)stream));
     }
-    if (!c->aux) {
-        HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_deep, hipEventDisableTiming));
-    }
     const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys};
     HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, B, cap, rows, cb, c->d_err, c->deep,
-                                     (hipStream_t)stream, e0, e1, c->aux, c->ev_scan, c->ev_deep, c->n_cu));
+                                     (hipStream_t)stream, e0, e1, c->n_cu));
     if (c1) HIPCHK(c, hipEventRecord(c1, (hipStream_t)stream));
     return PBG_OK;
 }

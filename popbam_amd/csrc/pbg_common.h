@@ -36,6 +36,13 @@ struct DevParams {
     // qfilter's rms test alone, for k = 0..16 keys: rms >= min_rmsQ iff sum mapQ^2 >= rmsq_thr[k]
     // (k = 0: rms is 0 -- the x86 NaN conversion -- so 0 when min_rmsQ <= 0, else never)
     uint32_t rmsq_thr[17];
+    // uniform tasks (call_scan_kernel's list pass, uniform_ref): d = 1..16 keys of one base m.
+    // uni_het[d][0 / 1] = the het m/x value with c_hi = 0 / d, (float)(-4.343 lhet[d<<8|c_hi])
+    // clamped at 0; uni_ok[d][cls] bit q (4..63) = the strand-free bound fk_prefix[d] *
+    // min_{q' >= q, c <= d-1} beta[q'][d][c] clears the smallest het m/x value (the margins of
+    // one_error_ref), cls 0: m = 0 (only c_hi = 0), 1: m = 3 (only c_hi = d), 2: m = 1, 2 (both)
+    float uni_het[17][2];
+    uint64_t uni_ok[17][3];
 };
 
 // Host-built tables resident in HBM for the lifetime of a context.
@@ -55,7 +62,7 @@ struct DevTables {
     // one-error tables in compact form (the scan kernel reads them through L1 / L2):
     // [0, 60 * 17) beta[q<<16|d<<8|0] at (q - 4) * 17 + d; then [60 * 17, 60 * 17 + 17 * 17)
     // lhet[n<<8|k] at 60 * 17 + n * 17 + k (n, k <= 16)
-    const double *oe;     // [60 * 17 + 17 * 17]
+    const double *oe;     // [kOeSize]
     const double *a1, *a2, *e1, *e2;          // Tajima/Fay-Wu constants (pop_sfs.cpp:511-571)
     const double *r2;     // concatenated per-population r^2 tables, see r2_off
     int32_t r2_off[PBG_MAX_POPS];             // offset of population p's (n_p+1)^3 table
@@ -252,13 +259,10 @@ struct Batch {
 };
 
 // kernel launchers (defined in call_kernel.hip / stats_kernel.hip)
-// aux (may be null): a second stream the deep-task queue kernel runs on, beside the shallow
-// one (they read disjoint queue ends); ev_scan / ev_deep order it after the scan and the fold
-// after it.  n_cu: the context device's CU count (sizes the persistent queue kernel's grid).
+// n_cu: the context device's CU count (sizes the persistent queue kernel's grid).
 hipError_t launch_call_sites(int row_bytes, const DevParams &P, const DevTables &T, const Batch &B, uint32_t cap,
                              void *rows, uint64_t *cb, int *err, const struct DeepBufs &D, hipStream_t stream,
-                             hipEvent_t ev0, hipEvent_t ev1, hipStream_t aux, hipEvent_t ev_scan, hipEvent_t ev_deep,
-                             int n_cu);
+                             hipEvent_t ev0, hipEvent_t ev1, int n_cu);
 size_t call_sites_lds_bytes(int n, uint32_t cap);
 // synthetic batch: k / rmsq / ref + per-block key totals, then an exclusive scan of the totals
 // into block_off (scratch: one u64 per 1024 blocks), then the keys

@@ -757,13 +757,16 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
 // intersection (the host's r^2 table); lanes past the row's end give +0.0, which leaves the sum
 // unchanged, so the adder sees the reference's exact sequence of additions.  Rounds run in
 // phases of kZnsR: while the adder sums phase k - 1 from one half of the ring, the producers
-// fill the other half with phase k; one workgroup barrier per phase.
+// fill the other half with phase k; one workgroup barrier per phase.  A producer first walks the
+// phase's kZnsR pairs (register arithmetic), then issues all their list reads, then all their
+// table reads, so a phase costs two LDS latencies, not 2 kZnsR.
 //
 // Fast path (every population of at most 32 samples and every list of the workgroup within the
 // LDS list capacity): the lists are staged in LDS as {population-compacted 32-bit mask,
-// popcount * (n_p + 1)} and the r^2 tables sit in LDS with a 0.0 slot past them, so a pair is
-// two LDS reads (the row's entry a broadcast), four VALU and the table read.  Otherwise the raw
-// masks (u64 / two-word) are read from the list buffer in HBM / L2, the table from LDS or HBM.
+// pc * (n_p + 1) | pc * (n_p + 1)^2 << 16} and the r^2 tables sit in LDS with a 0.0 slot past
+// them, so a pair is two LDS reads (the row's entry a broadcast), four VALU and the table read.
+// Otherwise the raw masks (u64 / two-word) are read from the list buffer in HBM / L2, the table
+// from LDS or HBM.
 constexpr int kZnsMaxC = 60;                 // chains per workgroup (64 + 16 C <= 1024 threads)
 constexpr int kZnsR = 4;                     // rounds per phase
 constexpr int kZnsRingStride = 18;           // doubles per (round, chain): 16 values + 2 pad (LDS banks)
@@ -852,7 +855,8 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
             const M *L = reinterpret_cast<const M *>(z.list);
             for (int b = lane; b < z.V; b += 64) {
                 const uint32_t m = compact32(L[b], pm);
-                s_lst[c * cap + b] = make_uint2(m, (uint32_t)__popc(m) * (uint32_t)z.np1);
+                const uint32_t pn = (uint32_t)__popc(m) * (uint32_t)z.np1;   // pc * (n_p + 1) | pc * (n_p + 1)^2 << 16
+                s_lst[c * cap + b] = make_uint2(m, pn | (pn * (uint32_t)z.np1) << 16);
             }
         }
     }
@@ -898,7 +902,7 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
     // ---- the producers: group c = (tid - 64) / 16 walks chain c, lane j takes pair (a, b0 + j)
     const int p = tid - 64, j = p & 15, c = p >> 4;
     const ZnsChain z = s_ch[c];
-    const int V = z.V, V1 = z.V - 1, np1 = z.np1, r2o = z.r2o;
+    const int V = z.V, V1 = z.V - 1, np1 = z.np1, r2o = z.r2o, vm = max(V1, 0);
     int a = 0, b0 = 1;
     const uint2 *lst = s_lst + c * cap;
     const M *L = reinterpret_cast<const M *>(z.list);
@@ -906,35 +910,50 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
     for (long long k = 0; k <= nphase; ++k) {
         if (k < nphase) {
             double *out = s_ring + (size_t)(k & 1) * kZnsR * rstride + (size_t)c * kZnsRingStride + j;
+            // the phase's pairs first (pure VALU), then every load of the phase in flight at once
+            int pa[kZnsR], pb[kZnsR];
+            bool ok[kZnsR];
+#pragma unroll
+            for (int r = 0; r < kZnsR; ++r) {
+                pa[r] = a;
+                pb[r] = b0 + j;
+                ok[r] = (a < V1) & (pb[r] < V);
+                b0 += 16;
+                const bool nxt = b0 >= V;
+                a += nxt ? 1 : 0;
+                b0 = nxt ? a + 1 : b0;
+            }
+            double v[kZnsR];
             if (fast) {
+                uint2 ea[kZnsR], eb[kZnsR];
 #pragma unroll
                 for (int r = 0; r < kZnsR; ++r) {
-                    const int b = b0 + j;
-                    const bool ok = (a < V1) & (b < V);
-                    const uint2 ea = lst[ok ? a : 0], eb = lst[ok ? b : 0];
-                    const int idx = ok ? r2o + (int)(ea.y * (uint32_t)np1 + eb.y) + __popc(ea.x & eb.x) : r2_lds;
-                    out[(size_t)r * rstride] = s_r2t[idx];
-                    b0 += 16;
-                    const bool nxt = b0 >= V;
-                    a += nxt ? 1 : 0;
-                    b0 = nxt ? a + 1 : b0;
+                    ea[r] = lst[min(pa[r], vm)];   // clamped, not selected: no branch (unused when !ok)
+                    eb[r] = lst[min(pb[r], vm)];
+                }
+#pragma unroll
+                for (int r = 0; r < kZnsR; ++r) {
+                    const int idx = r2o + (int)((ea[r].y >> 16) + (eb[r].y & 0xFFFFu)) + __popc(ea[r].x & eb[r].x);
+                    v[r] = s_r2t[ok[r] ? idx : r2_lds];
+                }
+            } else if (V > 1) {   // (a chain without pairs may have no list at all)
+                M ta[kZnsR], tb[kZnsR];
+#pragma unroll
+                for (int r = 0; r < kZnsR; ++r) {
+                    ta[r] = L[min(pa[r], vm)];
+                    tb[r] = L[min(pb[r], vm)];
+                }
+#pragma unroll
+                for (int r = 0; r < kZnsR; ++r) {
+                    const double x = tab[r2o + ((int)pc(ta[r]) * np1 + (int)pc(tb[r])) * np1 + (int)pc(ta[r] & tb[r])];
+                    v[r] = ok[r] ? x : 0.0;
                 }
             } else {
 #pragma unroll
-                for (int r = 0; r < kZnsR; ++r) {
-                    const int b = b0 + j;
-                    double v = 0.0;
-                    if ((a < V1) & (b < V)) {
-                        const M ta = L[a], tb = L[b];
-                        v = tab[r2o + ((int)pc(ta) * np1 + (int)pc(tb)) * np1 + (int)pc(ta & tb)];
-                    }
-                    out[(size_t)r * rstride] = v;
-                    b0 += 16;
-                    const bool nxt = b0 >= V;
-                    a += nxt ? 1 : 0;
-                    b0 = nxt ? a + 1 : b0;
-                }
+                for (int r = 0; r < kZnsR; ++r) v[r] = 0.0;
             }
+#pragma unroll
+            for (int r = 0; r < kZnsR; ++r) out[(size_t)r * rstride] = v[r];
         }
         __syncthreads();
     }
