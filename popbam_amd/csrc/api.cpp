@@ -241,22 +241,23 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
         // lower bound of the per-strand sum whatever the strands
         bool fk_dec = true;   // fk[n] = (1 - depcorr)^n (1 - eta) + eta (pop_utils.cpp:219) decreases
         for (int w = 1; w < 16; ++w) fk_dec = fk_dec && fk[w] <= fk[w - 1];
+        for (int i = 0; i < 17 * 3; ++i) d.uni[i] = 255u;
         for (int dd = 1; dd <= 16; ++dd) {
             float h[2];
-            for (int t = 0; t < 2; ++t) {
+            for (int t = 0; t < 2; ++t) {   // het m/x with c_hi = 0 / d: (float)(-4.343 lhet), clamped
                 const float v = (float)(-4.343 * lhet[dd << 8 | (t ? dd : 0)]);
                 h[t] = v < 0.0f ? 0.0f : v;
-                d.uni_het[dd][t] = h[t];
             }
             const float hm[3] = {h[0], h[1], std::min(h[0], h[1])};
             for (int cls = 0; cls < 3; ++cls) {
-                uint64_t bits = 0;
-                for (int q = 4; q < 64; ++q) {
+                uint32_t qthr = 255u;   // the bound grows with q_min (suffix minimum): first passing q
+                for (int q = 63; q >= 4; --q) {
                     const double lbv = lb[dd] * bu[(q - 4) * 17 + dd];
-                    if (fk_dec && hm[cls] > 0.0f && lbv * (1.0 - 1e-9) > (double)hm[cls] * (1.0 + 1e-6) + 1e-3)
-                        bits |= 1ull << q;
+                    if (fk_dec && hm[cls] > 0.0f && lbv * (1.0 - 1e-9) > (double)hm[cls] * (1.0 + 1e-6) + 1e-3) qthr = (uint32_t)q;
+                    else break;
                 }
-                d.uni_ok[dd][cls] = bits;
+                const uint32_t snpq = (uint32_t)(uint64_t)((double)hm[cls] + 0.499) & 0xFFFFu;
+                d.uni[dd * 3 + cls] = qthr | snpq << 8;
             }
         }
     }

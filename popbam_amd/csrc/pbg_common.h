@@ -36,13 +36,11 @@ struct DevParams {
     // qfilter's rms test alone, for k = 0..16 keys: rms >= min_rmsQ iff sum mapQ^2 >= rmsq_thr[k]
     // (k = 0: rms is 0 -- the x86 NaN conversion -- so 0 when min_rmsQ <= 0, else never)
     uint32_t rmsq_thr[17];
-    // uniform tasks (call_scan_kernel's list pass, uniform_ref): d = 1..16 keys of one base m.
-    // uni_het[d][0 / 1] = the het m/x value with c_hi = 0 / d, (float)(-4.343 lhet[d<<8|c_hi])
-    // clamped at 0; uni_ok[d][cls] bit q (4..63) = the strand-free bound fk_prefix[d] *
-    // min_{q' >= q, c <= d-1} beta[q'][d][c] clears the smallest het m/x value (the margins of
-    // one_error_ref), cls 0: m = 0 (only c_hi = 0), 1: m = 3 (only c_hi = d), 2: m = 1, 2 (both)
-    float uni_het[17][2];
-    uint64_t uni_ok[17][3];
+    // uniform tasks (call_scan_kernel's list pass, uniform_ref): d = 1..16 keys of one base m,
+    // uni[d * 3 + cls] (cls 0: m = 0, 1: m = 3, 2: m = 1 or 2) = the smallest q_min at which the
+    // strand-free bound fk_prefix[d] * min_{q' >= q_min, c <= d-1} beta[q'][d][c] clears the
+    // smallest het m/x value (the margins of one_error_ref; 255: never) | that value's snpq << 8
+    uint32_t uni[17 * 3];
 };
 
 // Host-built tables resident in HBM for the lifetime of a context.

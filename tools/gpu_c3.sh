@@ -11,11 +11,4 @@ rm -rf gpurun_out/c3/prof
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$R/gpurun_out/c3/prof" -o run \
   -- python3 "$R/bench.py" --config 3 --steps 1 --warmup 0 --cpu-sample 0 > gpurun_out/c3/prof.log 2>&1 || exit $?
 python3 tools/kstats.py gpurun_out/c3/prof/run_kernel_stats.csv
-i=0
-for set in FETCH_SIZE WRITE_SIZE; do
-  i=$((i+1)); rm -rf "gpurun_out/c3/pmc/p$i"
-  timeout -s KILL 300 rocprofv3 --pmc $set -T --output-format csv -d "$R/gpurun_out/c3/pmc/p$i" -o run \
-    -- python3 "$R/bench.py" --config 3 --steps 1 --warmup 0 --cpu-sample 0 > gpurun_out/c3/pmc/p$i.log 2>&1 \
-    || { echo "pmc pass $i failed"; exit 1; }
-done
-python3 tools/pmc_summary.py gpurun_out/c3/pmc > gpurun_out/c3/pmc/summary.txt && head -40 gpurun_out/c3/pmc/summary.txt
+bash tools/gpu_c3_pmc.sh
