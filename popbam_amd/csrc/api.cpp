@@ -364,7 +364,7 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         c->deep.task_cap = (uint32_t)std::min<size_t>(tcap, 0xFFFFFFFFu);
         c->deep.blk_cap = blk_cap;
         HIPCHK(c, hipMalloc((void **)&c->deep.blk_cnt, (size_t)nblk * sizeof(uint32_t)));
-        HIPCHK(c, hipMalloc((void **)&c->deep.raw, (size_t)nblk * blk_cap * sizeof(uint4)));
+        HIPCHK(c, hipMalloc((void **)&c->deep.raw, (size_t)nblk * blk_cap * 3 * sizeof(uint4)));
         c->deep_sites_cap = pl->n_sites;
         c->deep_info_cap = ntask;
     }

@@ -238,8 +238,8 @@ struct DeepBufs {
     uint32_t *blk_cnt;
     uint32_t blk_cap;
     uint64_t *pend;     // rows-only pipeline: per block, the positions whose row waits for a queued task
-    uint4 *raw;         // [nblk*blk_cap] queue records {site, sample | k << 8 | tried << 31, first key
-                        // (u64)}: call_slow_kernel re-reads the task's keys
+    uint4 *raw;         // [nblk*blk_cap*3] 48-byte queue records {site, sample | k << 8, sum mapQ^2,
+                        // reference byte} + the task's 16 keys (0 past k): all call_slow_kernel reads
 };
 #ifndef PBG_QGROUP
 #define PBG_QGROUP 16
