@@ -761,14 +761,14 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
 // phase's kZnsR pairs (register arithmetic), then issues all their list reads, then all their
 // table reads, so a phase costs two LDS latencies, not 2 kZnsR.
 //
-// Fast path (every population of at most 32 samples and every list of the workgroup within the
-// LDS list capacity): the lists are staged in LDS as {population-compacted 32-bit mask,
-// pc * (n_p + 1) | pc * (n_p + 1)^2 << 16} and the r^2 tables sit in LDS with a 0.0 slot past
-// them, so a pair is two LDS reads (the row's entry a broadcast), four VALU and the table read.
+// Fast path (every population of at most 26 samples and every list of the workgroup within the
+// LDS list capacity): the lists are staged in LDS as one u32 per site, the population-compacted
+// mask | popcount << 26, and the r^2 tables sit in LDS with a 0.0 slot past them, so a pair is
+// two LDS reads (the row's entry a broadcast), five VALU and the table read.
 // Otherwise the raw masks (u64 / two-word) are read from the list buffer in HBM / L2, the table
 // from LDS or HBM.
 constexpr int kZnsMaxC = 60;                 // chains per workgroup (64 + 16 C <= 1024 threads)
-constexpr int kZnsR = 4;                     // rounds per phase
+constexpr int kZnsR = 8;                     // rounds per phase
 constexpr int kZnsRingStride = 18;           // doubles per (round, chain): 16 values + 2 pad (LDS banks)
 
 // the sample bits of t inside population mask pm, packed to bit positions 0..pc(pm)-1
@@ -813,11 +813,11 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
     const int tid = (int)threadIdx.x, np = P.npops, nthr = (int)blockDim.x;
     const uint32_t nch = n_win * (uint32_t)np;
     const uint32_t ch0 = blockIdx.x * (uint32_t)C;
-    // LDS: r^2 tables (+ a 0.0 slot) | ring [2][kZnsR][C][kZnsRingStride] | lists [C][cap] uint2
+    // LDS: r^2 tables (+ a 0.0 slot) | ring [2][kZnsR][C][kZnsRingStride] | lists [C][cap] u32
     double *s_r2t = s_dyn;
     const int r2_slots = r2_lds ? ((r2_lds + 2) & ~1) : 0;
     double *s_ring = s_dyn + r2_slots;
-    uint2 *s_lst = reinterpret_cast<uint2 *>(s_ring + 2 * kZnsR * C * kZnsRingStride);
+    uint32_t *s_lst = reinterpret_cast<uint32_t *>(s_ring + 2 * kZnsR * C * kZnsRingStride);
     const size_t rstride = (size_t)C * kZnsRingStride;   // doubles per round
     if (tid == 0) {
         s_rounds = 0;
@@ -855,8 +855,7 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
             const M *L = reinterpret_cast<const M *>(z.list);
             for (int b = lane; b < z.V; b += 64) {
                 const uint32_t m = compact32(L[b], pm);
-                const uint32_t pn = (uint32_t)__popc(m) * (uint32_t)z.np1;   // pc * (n_p + 1) | pc * (n_p + 1)^2 << 16
-                s_lst[c * cap + b] = make_uint2(m, pn | (pn * (uint32_t)z.np1) << 16);
+                s_lst[c * cap + b] = m | (uint32_t)__popc(m) << 26;   // compacted mask | popcount << 26
             }
         }
     }
@@ -904,7 +903,8 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
     const ZnsChain z = s_ch[c];
     const int V = z.V, V1 = z.V - 1, np1 = z.np1, r2o = z.r2o, vm = max(V1, 0);
     int a = 0, b0 = 1;
-    const uint2 *lst = s_lst + c * cap;
+    const uint32_t *lst = s_lst + c * cap;
+    const uint32_t np1sq = (uint32_t)(np1 * np1);
     const M *L = reinterpret_cast<const M *>(z.list);
     const double *tab = r2_lds ? s_r2t : T.r2;
     for (long long k = 0; k <= nphase; ++k) {
@@ -925,7 +925,7 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
             }
             double v[kZnsR];
             if (fast) {
-                uint2 ea[kZnsR], eb[kZnsR];
+                uint32_t ea[kZnsR], eb[kZnsR];
 #pragma unroll
                 for (int r = 0; r < kZnsR; ++r) {
                     ea[r] = lst[min(pa[r], vm)];   // clamped, not selected: no branch (unused when !ok)
@@ -933,7 +933,8 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
                 }
 #pragma unroll
                 for (int r = 0; r < kZnsR; ++r) {
-                    const int idx = r2o + (int)((ea[r].y >> 16) + (eb[r].y & 0xFFFFu)) + __popc(ea[r].x & eb[r].x);
+                    const int idx = r2o + (int)(__umul24(ea[r] >> 26, np1sq) + __umul24(eb[r] >> 26, (uint32_t)np1)) +
+                                    __popc(ea[r] & eb[r] & 0x03FFFFFFu);
                     v[r] = s_r2t[ok[r] ? idx : r2_lds];
                 }
             } else if (V > 1) {   // (a chain without pairs may have no list at all)
@@ -984,14 +985,20 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
         const int r2_lds = r2_total <= 4608 ? r2_total : 0;   // <= 36 KB of LDS
         const uint32_t chains = n_win * (uint32_t)P.npops;
         // C chains per workgroup (64 + 16 C threads): two workgroups per CU when the chains allow
-        // it (two barrier domains interleave on a CU: 0.229 against 0.233 ms of statistics with one)
-        const int C = (int)std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)kZnsMaxC, (chains + 2 * n_cu - 1) / std::max(1, 2 * n_cu)));
-        const size_t fixed = (size_t)(r2_lds ? ((r2_lds + 2) & ~1) : 0) * 8 + (size_t)2 * kZnsR * C * kZnsRingStride * 8;
+        // it (two barrier domains interleave on a CU: 0.229 against 0.233 ms of statistics with
+        // one), and as many as the LDS budget holds with lists of up to 256 sites
         const size_t budget = 75 * 1024;   // LDS per workgroup: two per CU
-        int cap = budget > fixed ? (int)std::min<size_t>(4096, (budget - fixed) / ((size_t)C * 8)) & ~7 : 0;
-        const int compact = (max_pop <= 32 && r2_lds && cap >= 16) ? 1 : 0;
+        const size_t tab = (size_t)(r2_lds ? ((r2_lds + 2) & ~1) : 0) * 8;
+        const size_t per_chain = (size_t)2 * kZnsR * kZnsRingStride * 8 + 256 * 4;
+        const uint32_t cfit = budget > tab + per_chain ? (uint32_t)((budget - tab) / per_chain) : 1u;
+        const int C = (int)std::max<uint32_t>(1u, std::min<uint32_t>(std::min<uint32_t>((uint32_t)kZnsMaxC, cfit),
+                                                                      (chains + 2 * n_cu - 1) / std::max(1, 2 * n_cu)));
+        const size_t fixed = tab + (size_t)2 * kZnsR * C * kZnsRingStride * 8;
+        int cap = budget > fixed ? (int)std::min<size_t>(4096, (budget - fixed) / ((size_t)C * 4)) & ~7 : 0;
+        // fast path: compacted 26-bit masks (populations of at most 26 samples)
+        const int compact = (max_pop <= 26 && r2_lds && cap >= 16) ? 1 : 0;
         if (!compact) cap = 0;
-        const size_t lds = fixed + (size_t)C * cap * 8;
+        const size_t lds = fixed + (size_t)C * cap * 4;
         const dim3 g((chains + C - 1) / C), b(64 + 16 * C);
         if (rb == 16)
             hipLaunchKernelGGL(window_zns_kernel<M2>, g, b, lds, stream, P, T, n_win, A, r2_lds, C, cap, compact);
