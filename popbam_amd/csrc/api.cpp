@@ -743,7 +743,9 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         const int npairs = std::max(1, np * (np - 1));
         const size_t szw = nw, szp = (size_t)nw * np, szq = (size_t)nw * npairs, szn = (size_t)nw * n;
         const size_t szt = stats == PBG_S_TREE ? (size_t)nw * (n + 1) * (n + 1) : 1;
-        DevBuf o_ns, o_seg, o_d1, o_d2, o_d3, o_i1, o_i2, o_i3, o_td;
+        DevBuf o_ns, o_seg, o_d1, o_d2, o_d3, o_i1, o_i2, o_i3, o_td, o_bins;
+        const bool theta = stats == PBG_S_SFS && (cmd->output & 1);   // sfs --theta
+        const size_t szb = theta ? szp * (size_t)c->dp.sfs_stride : 1;
         HIPCHK(c, d_win.alloc(nw * sizeof(pbg_window)));
         HIPCHK(c, hipMemcpy(d_win.p, rw.data(), nw * sizeof(pbg_window), hipMemcpyHostToDevice));
         HIPCHK(c, o_ns.alloc(szw * 4));
@@ -755,6 +757,7 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         HIPCHK(c, o_i2.alloc(szp * 4));
         HIPCHK(c, o_i3.alloc(szq * 4));
         HIPCHK(c, o_td.alloc(szt * 4));
+        HIPCHK(c, o_bins.alloc(szb * 4));
         pbg_window_out O{};
         O.num_sites = (int32_t *)o_ns.p;
         O.segsites = (int32_t *)o_seg.p;
@@ -762,7 +765,10 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         int32_t *i1 = (int32_t *)o_i1.p, *i2 = (int32_t *)o_i2.p, *i3 = (int32_t *)o_i3.p;
         switch (stats) {
             case PBG_S_NUCDIV: O.pi = d1; O.dxy = d2; break;
-            case PBG_S_SFS: O.td = d1; O.fwh = d2; break;
+            case PBG_S_SFS:
+                O.td = d1; O.fwh = d2;
+                if (theta) { O.seg_pop = i1; O.theta_w = d3; O.sfs_bins = (int32_t *)o_bins.p; }
+                break;
             case PBG_S_ZNS: case PBG_S_OMEGA: O.ld_snps = i1; O.ld_val = d1; break;
             case PBG_S_WALL: O.ld_snps = i1; O.ld_val = d1; O.ld_q = d2; break;
             case PBG_S_DIV_IND: O.div_ind = d1; break;
@@ -792,6 +798,8 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
         HIPCHK(c, hipMemcpy(h_i2.data(), o_i2.p, szp * 4, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_i3.data(), o_i3.p, szq * 4, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_td.data(), o_td.p, szt * 4, hipMemcpyDeviceToHost));
+        std::vector<int32_t> h_bins(szb);
+        HIPCHK(c, hipMemcpy(h_bins.data(), o_bins.p, szb * 4, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_d1.data(), o_d1.p, h_d1.size() * 8, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_d2.data(), o_d2.p, h_d2.size() * 8, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(h_d3.data(), o_d3.p, h_d3.size() * 8, hipMemcpyDeviceToHost));
@@ -807,7 +815,16 @@ long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, si
             };
             switch (stats) {
                 case PBG_S_NUCDIV: wh.pi = slice(h_d1, i * np, np); wh.dxy = slice(h_d2, i * npairs, npairs); break;
-                case PBG_S_SFS: wh.td = slice(h_d1, i * np, np); wh.fwh = slice(h_d2, i * np, np); break;
+                case PBG_S_SFS:
+                    wh.td = slice(h_d1, i * np, np); wh.fwh = slice(h_d2, i * np, np);
+                    if (theta) {
+                        wh.seg_pop = slice(h_i1, i * np, np); wh.theta_w = slice(h_d3, i * np, np);
+                        wh.sfs_bins.assign(np, {});
+                        for (int p = 0; p < np; ++p)
+                            wh.sfs_bins[p] = slice(h_bins, ((size_t)i * np + p) * c->dp.sfs_stride,
+                                                   (size_t)c->dp.pop_n[p] + 1);
+                    }
+                    break;
                 case PBG_S_ZNS: case PBG_S_OMEGA:
                     wh.ld_snps = slice(h_i1, i * np, np); wh.ld_val = slice(h_d1, i * np, np); break;
                 case PBG_S_WALL:
@@ -876,6 +893,13 @@ long pbg_format(const pbg_ctx *c, const pbg_cmd *cmd, const pbg_window_out *ho, 
         wh.hap_dxy = take(ho->hap_dxy, (size_t)i * npairs, npairs);
         wh.hap_min = take(ho->hap_min, (size_t)i * npairs, npairs);
         wh.tree_diff = take(ho->tree_diff, (size_t)i * (n + 1) * (n + 1), (size_t)(n + 1) * (n + 1));
+        if (cmd->cmd == PBG_CMD_SFS && (cmd->output & 1) && ho->seg_pop && ho->theta_w && ho->sfs_bins) {
+            wh.seg_pop = take(ho->seg_pop, (size_t)i * np, np);
+            wh.theta_w = take(ho->theta_w, (size_t)i * np, np);
+            wh.sfs_bins.assign(np, {});
+            for (int p = 0; p < np; ++p)
+                wh.sfs_bins[p] = take(ho->sfs_bins, ((size_t)i * np + p) * c->dp.sfs_stride, (size_t)c->dp.pop_n[p] + 1);
+        }
         pbg::format_window(text, *cmd, n, np, c->dp.flag, wh);
     }
     if (needed) *needed = text.size() + 1;

@@ -264,6 +264,20 @@ void format_window(std::string &out, const pbg_cmd &c, int n, int np, uint32_t f
                 o.t("\tH[" + pn(c, i) + "]:\t");
                 if (std::isnan(w.fwh[i])) o.na(); else o.f(w.fwh[i]);
             }
+            // --theta: the integers and theta_W calc_sfs computes but print_sfs never prints,
+            // appended after the reference's columns so the default output is unchanged
+            if ((c.output & 1) && (int)w.seg_pop.size() == np && (int)w.sfs_bins.size() == np)
+                for (int i = 0; i < np; i++) {
+                    o.t("\tS[" + pn(c, i) + "]:\t");
+                    o.i(w.seg_pop[i]);
+                    o.t("\tthetaW[" + pn(c, i) + "]:\t");
+                    if (!std::isfinite(w.theta_w[i])) o.na(); else o.f(w.theta_w[i]);
+                    o.t("\tsfs[" + pn(c, i) + "]:\t");
+                    for (size_t j = 0; j < w.sfs_bins[i].size(); j++) {
+                        if (j) o.t(",");
+                        o.i(w.sfs_bins[i][j]);
+                    }
+                }
             break;
         case PBG_CMD_LD:  // print_ld pop_ld.cpp:650-712
             for (int i = 0; i < np; i++) {

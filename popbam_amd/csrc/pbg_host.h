@@ -20,6 +20,11 @@ struct WindowHost {
     int32_t num_sites = 0, segsites = 0;
     std::vector<double> pi, dxy, td, fwh, ld_val, ld_q, div_ind, div_pop, hap_val, hap_dxy;
     std::vector<int32_t> ld_snps, div_fixed, div_seg, nhaps, hap_min, tree_diff;
+    // sfs --theta (pbg_cmd.output bit 0): calc_sfs's S, Watterson's theta and the spectrum
+    // sfs[0..n_pop] per population (pop_sfs.cpp:246-263)
+    std::vector<int32_t> seg_pop;
+    std::vector<double> theta_w;
+    std::vector<std::vector<int32_t>> sfs_bins;
 };
 
 // print_nucdiv / print_sfs / print_ld / print_diverge / print_haplo (TSV, byte-identical)

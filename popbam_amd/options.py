@@ -183,6 +183,8 @@ def parse_args(cmd: str, argv: list[str]) -> Options:
         o.flag |= BAM_MINPOPSAMPLE
     if cmd == "diverge" and "t" in present:
         o.flag |= BAM_SUBSTITUTE
+    if cmd == "sfs" and "--theta" in argv:
+        o.output |= 1   # extension: append S, theta_W and the spectrum (print_sfs never prints them)
     if cmd == "ld" and "e" in present:
         o.min_freq = 2
     if cmd == "snp" and "v" in present:

@@ -170,3 +170,43 @@ def test_fatal_errors_before_the_gpu(capsys, tmp_path):
     assert rc == 1 and f"Index file not available for BAM file {noidx}" in err
     rc, out, err = _main(["nucdiv", "-f", str(tmp_path / "none.fa"), bam, "chr1"], capsys)
     assert rc == 1 and "Failed to load index for fastA reference file" in err
+
+
+THETA_CASES = [("g01_base", 1), ("g03_threepops", 1), ("g04_outgroup", 0), ("g12_regions", 2), ("g15_24s3p", 22),
+               ("g18_64s4p", 15), ("g01_base", 18)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,idx", THETA_CASES, ids=[f"{n}-{i:02d}" for n, i in THETA_CASES])
+def test_cli_sfs_theta_extension(gpu_lib, name, idx):
+    """`popbam sfs --theta` (an extension: calc_sfs, pop_sfs.cpp:246-263, computes S and the
+    spectrum but print_sfs never prints them): the reference's columns stay byte-identical and
+    the appended S[p] / thetaW[p] / sfs[p] columns are consistent: S = sum of bins 1..n-1 and
+    theta_W = S / a1[n] (calc_a1, pop_sfs.cpp:511-525).  The bins themselves are pinned against
+    the oracle's calc_sfs integers by test_gpu_scale.py::test_sfs_bins_and_theta_w."""
+    import re
+    cs = fixtures.load_case(name)["meta"]["cases"][idx]
+    argv = _argv(name, cs)
+    ours = cli.run(argv[0], argv[1:] + ["--theta"])
+    gold = fixtures.golden_text(name, cs["stdout"])
+    lines, glines = ours.splitlines(), gold.splitlines()
+    assert len(lines) == len(glines) and lines
+    seen = 0
+    for ln, gl in zip(lines, glines):
+        assert ln.startswith(gl + "\tS["), (gl, ln)
+        ext = ln[len(gl):].split("\t")[1:]
+        assert len(ext) % 6 == 0
+        for j in range(0, len(ext), 6):
+            pop = re.fullmatch(r"S\[(.+)\]:", ext[j]).group(1)
+            assert ext[j + 2] == f"thetaW[{pop}]:" and ext[j + 4] == f"sfs[{pop}]:"
+            s = int(ext[j + 1])
+            bins = [int(b) for b in ext[j + 5].split(",")]
+            n = len(bins) - 1
+            assert s == sum(bins[1:n]) and min(bins) >= 0
+            a1 = sum(1.0 / i for i in range(1, n))
+            if ext[j + 3].strip() == "NA":
+                assert n < 2
+            else:
+                assert abs(float(ext[j + 3]) - s / a1) <= 5e-6, (ext[j + 3], s, a1)
+            seen += s
+    assert seen > 0
