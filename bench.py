@@ -30,7 +30,46 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 METRIC = "Msites/sec (nucdiv+sfs+ld, 10kb win, 12 samples) at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-LAYOUT = "keys16"       # pileup batch layout the committed PMC profile was taken on
+CALL_KERNELS = ("call_scan_kernel", "call_slow_kernel", "call_deepq_kernel", "call_overflow_kernel",
+                "call_pend_fold_kernel")
+
+
+def source_hash() -> str:
+    """sha256 over the sources libpopbam_gpu.so is built from (popbam_amd/csrc, include): a PMC
+    profile counts for this build only if it records the same hash."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(REPO, "popbam_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(REPO, "popbam_amd", "csrc", "*.cpp")) +
+                   glob.glob(os.path.join(REPO, "popbam_amd", "csrc", "*.h")) +
+                   [os.path.join(REPO, "popbam_amd", "csrc", "Makefile")] +
+                   glob.glob(os.path.join(REPO, "include", "*.h")))
+    for f in files:
+        h.update(os.path.relpath(f, REPO).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(config: int, shape: dict) -> dict | None:
+    """Per-launch HBM bytes of the call kernels from rocprofv3 counters (FETCH_SIZE x 2 +
+    WRITE_SIZE, separate --pmc passes; tools/pmc_traffic.py), accepted only when the profile
+    was taken on this source tree (same source_hash) and this shape; else None."""
+    path = os.path.join(REPO, "profiles", f"pmc_traffic_c{config}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except Exception:
+        return None
+    if d.get("src_sha") != source_hash():
+        return None
+    if any(d.get("shape", {}).get(k) != v for k, v in shape.items()):
+        return None
+    d["file"] = os.path.relpath(path, REPO)
+    return d
 
 
 def parse():
@@ -45,11 +84,14 @@ def parse():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xC0FFEE02)
     ap.add_argument("--cpu-sample", type=int, default=60_000, help="positions for the CPU port baseline (0 = skip all)")
     ap.add_argument("--ref-sample", type=int, default=200_000, help="positions for the reference-binary baseline")
-    ap.add_argument("--e2e-chunk", type=int, default=4_000_000,
-                    help="config 2: positions per chunk of the measured host-input pass (0 = skip)")
+    ap.add_argument("--e2e-chunk", type=int, default=0,
+                    help="config 2: positions per device slot of the measured host-input run (0 = the library's "
+                         "default, -1 = skip)")
     ap.add_argument("--e2e-passes", type=int, default=2)
     ap.add_argument("--cli-sample", type=int, default=200_000,
                     help="config 2: positions of the BAM the drop-in CLI is timed on (0 = skip)")
+    ap.add_argument("--parity-windows", type=int, default=20,
+                    help="after timing: windows of the run checked against the CPU oracle (0 = skip)")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
                     help="BASELINE.json configs[i]: 2 = 50 Msites x 12 samples (the metric's config), "
                          "3 = whole genome 24 contigs x 125 Mbp x 24 samples, nucdiv+sfs+ld+diverge, "
@@ -197,35 +239,90 @@ def pcie_rate(torch, batch_bytes: int, step_s: float, sites: int) -> dict:
             "Msites_per_s_overlapped": round(sites / max(copy_s, step_s) / 1e6, 2)}
 
 
-def end_to_end(args, torch, hp, stream) -> dict:
-    """Measured host-input rate: the same contig handed over in
-    pinned HOST memory, streamed host -> device in chunks of whole windows on a copy stream
-    while the previous chunk is called and its windows computed (workload.HostStream, double
-    buffered); wall time of whole passes.  The pass's rows and window outputs are checked
-    against the HBM-resident step's."""
-    want_rows = hp.rows.clone()
-    want = {k: hp.out.t[k].clone() for k in ("num_sites", "segsites", "pi", "td", "ld_val")}
+def stat_cmds(args, n: int, n_pops: int, lo: int, hi: int):
+    """PbgCmd structures for `popbam nucdiv|sfs|ld -w <window>` over [lo, hi) (the metric's three
+    commands) and the names they point at (kept alive by the caller)."""
+    from popbam_amd import _lib
+    keep = [b"chr1", (C.c_char_p * n)(*[f"s{i}".encode() for i in range(n)]),
+            (C.c_char_p * n_pops)(*[f"p{i}".encode() for i in range(n_pops)])]
+    cmds = []
+    for cmd_id in (4, 6, 5):   # nucdiv, sfs, ld (popbam_func_t)
+        c = _lib.PbgCmd()
+        c.cmd, c.output, c.min_sites, c.min_snps, c.min_freq = cmd_id, 0, 10, 10, 1
+        c.windowed, c.win_size, c.beg, c.end = 1, args.window, lo, hi
+        c.chr_name = keep[0]
+        c.sample_names = C.cast(keep[1], C.POINTER(C.c_char_p))
+        c.pop_names = C.cast(keep[2], C.POINTER(C.c_char_p))
+        c.refid = b"ref"
+        cmds.append(c)
+    return cmds, keep
+
+
+def resident_texts(ctx, hp, cmds, wins) -> list:
+    """print_<stat> of the HBM-resident step's window outputs (pbg_format) for each command."""
+    import numpy as np
+    from popbam_amd import _lib
+    host = {k: v.cpu().numpy() for k, v in hp.out.t.items()}
+    o = _lib.PbgWindowOut()
+    for k, _ in _lib.PbgWindowOut._fields_:
+        setattr(o, k, host[k].ctypes.data)
+    wb = np.array([a for a, _ in wins], np.int32)
+    we = np.array([b for _, b in wins], np.int32)
+    out = []
+    for c in cmds:
+        need = C.c_size_t(0)
+        ctx.lib.pbg_format(ctx.h, C.byref(c), C.byref(o), len(wins), wb.ctypes.data, we.ctypes.data, None, 0, C.byref(need))
+        buf = C.create_string_buffer(need.value)
+        ctx.check(ctx.lib.pbg_format(ctx.h, C.byref(c), C.byref(o), len(wins), wb.ctypes.data, we.ctypes.data, buf,
+                                     need.value, C.byref(need)), "pbg_format")
+        out.append(buf.value.decode())
+    return out
+
+
+def end_to_end(args, torch, ctx, hp, wins) -> dict:
+    """Measured host-input rate through the C-ABI: the contig's key
+    batch handed over in pinned HOST memory to a streamed run (pbg_stream_open / _push /
+    _finish: chunks copied host -> device on a copy stream into two device slots while the
+    previous chunk is called, then nucdiv + sfs + ld over every window and their TSV), wall time
+    of whole runs, open to text.  The run's rows and texts are checked against the HBM-resident
+    step's (rows bit for bit, texts byte for byte)."""
+    from popbam_amd import _lib
+    n, np_ = ctx.params.n_samples, ctx.params.n_pops
+    cmds, keep = stat_cmds(args, n, np_, 0, args.sites)
+    want = resident_texts(ctx, hp, cmds, wins)
     host = hp.to_host()
-    hs = hp.host_stream(host, args.e2e_chunk, args.window)
-    hp.rows.zero_()
-    for k in want:
-        hp.out.t[k].zero_()
-    hs.run(stream)   # warmup pass (plans, slots)
+    piece = _lib.PbgPileup(args.sites, 0, host["ref"].data_ptr(), host["k"].data_ptr(), host["rmsq"].data_ptr(),
+                           host["block_off"].data_ptr(), host["keys"].data_ptr())
+
+    def run():
+        with _lib.Stream(ctx, cmds, 0, args.sites, args.e2e_chunk) as st:
+            st.push(piece)
+            st.finish()
+            return st, [st.text(i) for i in range(len(cmds))], st.profile()
+
+    rows = torch.empty_like(hp.rows)
+    with _lib.Stream(ctx, cmds, 0, args.sites, args.e2e_chunk) as st:   # warmup: slots, plans
+        st.push(piece)
+        st.finish()
+        st.rows_into(rows.data_ptr(), rows.numel())
+        texts = [st.text(i) for i in range(len(cmds))]
     torch.cuda.synchronize()
-    same = bool(torch.equal(hp.rows, want_rows)) and all(bool(torch.equal(hp.out.t[k], v)) for k, v in want.items())
+    same = bool(torch.equal(rows, hp.rows)) and texts == want
     passes = max(1, args.e2e_passes)
     t0 = time.perf_counter()
     for _ in range(passes):
-        hs.run(stream)
-    torch.cuda.synchronize()
+        _, texts, prof = run()
     dt = (time.perf_counter() - t0) / passes
+    same = same and texts == want
     del host
-    return {"Msites_per_s": round(args.sites / dt / 1e6, 2), "ms_per_pass": round(dt * 1e3, 2),
-            "h2d_bytes_per_pass": hs.h2d_bytes, "h2d_GBps_effective": round(hs.h2d_bytes / dt / 1e9, 2),
-            "chunk_sites": hs.chunk, "chunks": len(hs.chunks), "passes": passes,
-            "matches_resident": same,
-            "how": "pinned host batch (SURVEY 8(d) layout) -> H2D on a copy stream into two device slots, "
-                   "pbg_call_sites + pbg_window_stats per chunk on the compute stream; wall time per pass"}
+    return {"Msites_per_s": round(args.sites / dt / 1e6, 2), "ms_per_run": round(dt * 1e3, 2),
+            "h2d_bytes_per_run": prof["h2d_bytes"], "h2d_GBps_effective": round(prof["h2d_bytes"] / dt / 1e9, 2),
+            "chunks": prof["chunks"], "pinned_chunks": prof["pinned_chunks"],
+            "ms_h2d_device": round(prof["ms_h2d"], 2), "ms_call_device": round(prof["ms_call"], 2),
+            "ms_finish": round(prof["ms_finish"], 2), "runs": passes, "matches_resident": same,
+            "how": "C-ABI pbg_stream_*: pinned host key batch (SURVEY 8(d) layout) -> H2D chunks on a copy stream "
+                   "into two device slots, pbg_call_sites per chunk on the compute stream, then nucdiv + sfs + ld "
+                   "over all windows and their TSV; wall time per run (open -> three texts)"}
 
 
 def cli_rate(args) -> dict:
@@ -271,6 +368,63 @@ def cli_rate(args) -> dict:
                 "note": "3 commands summed, as the CPU baseline; a fresh process pays Python + torch import and "
                         "context creation; in-process is the feeder + GPU path alone"})
     return res
+
+
+def parity_sampled_resident(args, ctx, hp, wins, contig: int) -> dict:
+    """Checker (outside the timed region): --parity-windows windows of the timed configs[2] step,
+    drawn at random, compared with the CPU oracle (tests/parity_sample.py): the rows of their
+    positions bit for bit, their printed statistics byte for byte."""
+    import parity_sample as ps
+    rb = ctx.row_bytes
+    idx = ps.pick(len(wins), args.parity_windows, args.seed ^ 0x5A5A)
+    fields = hp.fields_for(hp.stats)
+    picks = []
+    for i in idx:
+        a, b = wins[i]
+        one = {}
+        for k in fields:
+            t = hp.out.t[k]
+            per = t.numel() // max(1, len(wins))
+            one[k] = t[i * per:(i + 1) * per].cpu().numpy()
+        picks.append((contig, a, b, hp.rows[a * rb:b * rb].cpu().numpy(), one))
+    t0 = time.perf_counter()
+    r = ps.check_windows(ctx, ctx.params, picks, args.seed, args.depth, hp.stats)
+    r["seconds"] = round(time.perf_counter() - t0, 2)
+    return r
+
+
+def parity_sampled_genome(args, ctx, gp, k: int) -> dict:
+    """The same check on windows of a streamed configs[3] / [4] pass (rows of every chunk stay
+    resident; window outputs per row group)."""
+    import parity_sample as ps
+    from popbam_amd import workload
+    rb = ctx.row_bytes
+    fields = workload.HotPath.fields_for(gp.stats)
+    flat = []   # (segment, local window) in segment order = the order of gp.gstats' windows
+    for si, w in enumerate(gp.win_lists):
+        flat += [(si, j) for j in range(len(w))]
+    where = []  # (group, index in group) in the same order
+    for g, (_, _, _, nw, _, _) in enumerate(gp.gstats):
+        where += [(g, j) for j in range(nw)]
+    idx = ps.pick(len(flat), k, args.seed ^ 0x5A5A)
+    picks = []
+    for i in idx:
+        si, j = flat[i]
+        s = gp.segments[si]
+        a, b = gp.win_lists[si][j]
+        g, li = where[i]
+        out, nw = gp.gstats[g][4], gp.gstats[g][3]
+        one = {}
+        for f in fields:
+            t = out.t[f]
+            per = t.numel() // max(1, nw)
+            one[f] = t[li * per:(li + 1) * per].cpu().numpy()
+        rows = gp.segment_rows(si)[a * rb:b * rb].cpu().numpy()
+        picks.append((s.contig, s.beg + a, s.beg + b, rows, one))
+    t0 = time.perf_counter()
+    r = ps.check_windows(ctx, ctx.params, picks, args.seed, args.depth, gp.stats)
+    r["seconds"] = round(time.perf_counter() - t0, 2)
+    return r
 
 
 def max_over_ranks(dist, x: float) -> float:
@@ -340,6 +494,11 @@ def bench_genome(args, torch, dist, world, rank):
     ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
     scan_ms_alone = k1.value / max(1, n1.value)
     achieved_alone = sb0 / (scan_ms_alone * 1e-3) / 1e9
+    pmc = pmc_traffic(args.config, {"contigs": args.contigs, "contig_len": args.contig_len, "samples": n,
+                                    "depth": args.depth, "chunk": args.chunk, "world": world})
+    traffic = pmc["kernels"]["call_scan_kernel"]["hbm_bytes"] if pmc else None
+    call_traffic = sum(pmc["kernels"].get(k, {}).get("hbm_bytes", 0) for k in CALL_KERNELS) if pmc else None
+    bpl = sb // max(1, chunks)
     out = None
     if rank == 0:
         value = total_sites * args.steps / elapsed / 1e6
@@ -360,7 +519,12 @@ def bench_genome(args, torch, dist, world, rank):
                        "chunks_rank0": chunks, "parallelism": f"dp{world} (contig-first shards, no collective)"},
             "roofline": {"bound": "hbm", "kernel": "call_scan_kernel", "achieved": round(achieved_pass, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_pass / HBM_PEAK_GBS, 4),
-                         "traffic": None, "bytes_per_launch": sb // max(1, chunks), "ms_per_launch": round(scan_ms, 4),
+                         "traffic": traffic, "bytes_per_launch": bpl, "ms_per_launch": round(scan_ms, 4),
+                         "traffic_ratio": round(traffic / bpl, 4) if traffic else None,
+                         "call_stage_traffic": call_traffic,
+                         "traffic_source": (f"{pmc['file']} (src_sha {pmc['src_sha']}, {pmc['source']}; mean over the "
+                                            f"pass's chunk launches)" if pmc else
+                                            "no PMC profile of this source tree (tools/pmc_traffic.sh)"),
                          "bytes_basis": "SURVEY 8(d): sum over (position, sample) of 2k+5, +1 +row_bytes per position",
                          "measured_on": (f"every chunk launch of the timed pass ({chunks} per pass; library HIP "
                                          "events on the call stream)") +
@@ -379,6 +543,11 @@ def bench_genome(args, torch, dist, world, rank):
         out["cpu_baseline"] = cpu_baseline(args) if (world == 1 and args.cpu_sample > 0) else None
         if out["cpu_baseline"]:
             out["x_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+        if args.parity_windows > 0:
+            ps = parity_sampled_genome(args, ctx, gp, max(4, args.parity_windows // (2 if args.config == 3 else 1)))
+            out["parity_sampled"] = ps["ok"]
+            out["parity_sample"] = ps
+        out["src_sha"] = source_hash()
         print(json.dumps(out), flush=True)
     ctx.close()
 
@@ -473,18 +642,10 @@ def main():
     achieved = scan_bytes * args.steps / (kt.value * 1e-3) / 1e9
     stats_bytes = args.sites * ctx.row_bytes
 
-    # per-launch HBM traffic from rocprofv3 PMC counters, when a profile of this code is committed
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_call_scan_kernel.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                d = json.load(f)
-            if (d.get("sites") == args.sites and d.get("samples") == n and d.get("depth") == args.depth
-                    and d.get("layout") == LAYOUT and d.get("pieces", 1) == len(pts) - 1):
-                traffic = d.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    # per-launch HBM traffic from rocprofv3 PMC counters of this source tree (else null)
+    pmc = pmc_traffic(2, {"sites": args.sites, "samples": n, "depth": args.depth, "pieces": len(pts) - 1})
+    traffic = pmc["kernels"]["call_scan_kernel"]["hbm_bytes"] if pmc else None
+    call_traffic = sum(pmc["kernels"].get(k, {}).get("hbm_bytes", 0) for k in CALL_KERNELS) if pmc else None
 
     out = None
     if rank == 0:
@@ -504,27 +665,37 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "call_scan_kernel", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "bytes_per_launch": scan_bytes_launch, "ms_per_launch": round(scan_ms, 4),
+                         "traffic_ratio": round(traffic / scan_bytes_launch, 4) if traffic else None,
+                         "traffic_source": (f"{pmc['file']} (src_sha {pmc['src_sha']}, {pmc['source']})" if pmc else
+                                            "no PMC profile of this source tree (tools/pmc_traffic.sh)"),
                          "bytes_basis": "SURVEY 8(d): sum over (position, sample) of 2k+5, +1 +row_bytes per position",
                          "layout_bytes_per_launch": layout_bytes,
                          "frac_layout": round(layout_bytes * args.steps / (kt.value * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "call_stage": {"ms_serial": round(call_ms, 4), "ms_library_events": round(call_lib_ms, 4),
                            "bytes": call_bytes, "GBps": round(call_bytes / (call_lib_ms * 1e-3) / 1e9, 2),
                            "frac": round(call_bytes / (call_lib_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                           "kernels": "call_scan + call_slow + call_deepq + call_overflow + call_fold"},
+                           "kernels": "call_scan + call_slow + call_deepq + call_overflow + call_fold",
+                           "traffic": call_traffic,
+                           "traffic_ratio": round(call_traffic / call_bytes, 4) if call_traffic else None},
             "window_stats": {"ms_serial": round(stats_ms, 4), "rows_bytes": stats_bytes,
                              "GBps": round(stats_bytes / (stats_ms * 1e-3) / 1e9, 2),
                              "Msites_per_s_stats_only": round(args.sites / (stats_ms * 1e-3) / 1e6, 2)},
         }
         if world == 1:
             out["pcie_inclusive"] = pcie_rate(torch, layout_bytes - args.sites * n, elapsed / args.steps, args.sites)
-            if args.e2e_chunk > 0 and args.cpu_sample > 0:   # --cpu-sample 0 (profiling runs) skips the extras
-                out["end_to_end"] = end_to_end(args, torch, hp, stream)
+            if args.e2e_chunk >= 0 and args.cpu_sample > 0:   # --cpu-sample 0 (profiling runs) skips the extras
+                out["end_to_end"] = end_to_end(args, torch, ctx, hp, wins)
             if args.cli_sample > 0 and args.cpu_sample > 0:
                 out["cli"] = cli_rate(args)
         if world == 1 and args.cpu_sample > 0:
             out["cpu_baseline"] = cpu_baseline(args)
         else:
             out["cpu_baseline"] = None
+        if args.parity_windows > 0:
+            ps = parity_sampled_resident(args, ctx, hp, wins, rank)
+            out["parity_sampled"] = ps["ok"]
+            out["parity_sample"] = ps
+        out["src_sha"] = source_hash()
         print(json.dumps(out), flush=True)
     ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
     ctx.close()

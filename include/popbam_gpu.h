@@ -90,7 +90,8 @@ typedef struct {
  *                 it from k[] when NULL)
  *   keys[]        one u16 per kept read, (position, sample, pileup order) major:
  *                 qq<<5 | strand<<4 | base (popbam.cpp:284), qq = clamp(min(baseQ, mapQ), 4, 63)
- * Device batches: keys[] must be 16-byte aligned (any hipMalloc / torch allocation is).
+ * Device batches: keys[], k[] and rmsq[] must be 16-byte aligned (any hipMalloc / torch
+ * allocation is; the kernels read them with 16-byte loads).
  * block_off[0] need not be 0: the kernels read only the 16-byte chunks of keys[] that hold
  * keys [block_off[0], block_off[last]), so a caller may pass keys shifted back by a
  * multiple of 8 keys to address a buffer that holds only that range.                     */
@@ -223,7 +224,8 @@ typedef struct {
 
 /* Runs `popbam <cmd>` over a HOST pileup batch that covers contig positions
  * [pileup->pos0, pileup->pos0 + n_sites) (host pointers; block_off may be NULL and is then
- * derived from k[]).  Writes the reference's stdout (TSV) into out (NUL-terminated).
+ * derived from k[]): one stream (pbg_stream_*, below) over the 64-position blocks the
+ * command's windows touch.  Writes the reference's stdout (TSV) into out (NUL-terminated).
  * Returns the text length, or PBG_E_RANGE with *needed set when cap is too small; the text
  * is then kept by the context and pbg_take_text() copies it without running again.       */
 long pbg_run(pbg_ctx *ctx, const pbg_cmd *cmd, const pbg_pileup *host_pileup, char *out,
@@ -235,6 +237,49 @@ long pbg_take_text(pbg_ctx *ctx, char *out, size_t cap);
  * prints (+1 applied here).  Same return convention as pbg_run.                          */
 long pbg_format(const pbg_ctx *ctx, const pbg_cmd *cmd, const pbg_window_out *host_out, uint32_t n_win,
                 const int32_t *wbeg, const int32_t *wend, char *out, size_t cap, size_t *needed);
+
+/* ---- streamed runs over HOST batches ------------------------------------------------- */
+/* The host side of the pileup callback produces a region's key batch position by position; a
+ * stream takes it in pieces, in position order, while the walk goes on (the reference instead
+ * re-fetches and re-piles every window, pop_nucdiv.cpp:57-125, and calls each position inside
+ * the callback).  Each pushed piece is copied to the device in chunks that alternate between
+ * two device slots (the copy of chunk i+1 runs under the call of chunk i) and called into the
+ * region's rows; pbg_stream_finish then runs every command's windows (main_<cmd>'s window loop)
+ * over those rows and prints their TSV.  Slots, pinned staging, the rows buffer and the window
+ * lists (with their statistics plans) belong to the context and serve the next stream: a steady
+ * state of streams allocates nothing.  One open stream per context; pbg_run is one stream of
+ * one command over one piece.
+ *   cmds         the commands to print (all over the same region; the pointers inside them --
+ *                names -- must stay valid until pbg_stream_finish); snp -o 0 keeps consensus words
+ *   pos0,n_sites the region [pos0, pos0 + n_sites) of contig positions the pieces cover
+ *   chunk_sites  positions per device slot (0: about 256 MB of pileup per slot)
+ * A piece (host pointers, block_off may be NULL: derived from k[]) starts where the previous
+ * one ended and holds a multiple of 64 positions unless it is the last.  Pageable buffers are
+ * copied before pbg_stream_push returns; pinned ones (hipHostMalloc / hipHostRegister) are read
+ * by DMA asynchronously and must stay unchanged until pbg_stream_finish.                     */
+typedef struct pbg_stream pbg_stream;
+typedef struct {
+    uint64_t h2d_bytes;      /* bytes copied host -> device                                   */
+    uint32_t pieces, chunks; /* pushes; device chunks                                          */
+    uint32_t pinned_chunks;  /* chunks copied straight from pinned caller buffers              */
+    uint32_t _pad;
+    double   ms_stage;       /* host: pageable pieces -> pinned staging (threaded memcpy)      */
+    double   ms_wait;        /* host: waiting for a slot's previous copy                       */
+    double   ms_h2d;         /* device: the chunks' H2D copies (events on the copy stream)     */
+    double   ms_call;        /* device: pbg_call_sites per chunk (events on the compute stream) */
+    double   ms_finish;      /* host: pbg_stream_finish (wait, statistics, D2H, printing)      */
+} pbg_stream_prof;
+int  pbg_stream_open(pbg_ctx *ctx, const pbg_cmd *cmds, uint32_t n_cmd, int32_t pos0, uint32_t n_sites,
+                     uint32_t chunk_sites, pbg_stream **st);
+int  pbg_stream_push(pbg_stream *st, const pbg_pileup *host_piece);
+int  pbg_stream_finish(pbg_stream *st);   /* waits, checks (PBG_E_BATCH ...), prints every command */
+/* command i's text (NUL-terminated); returns its length or PBG_E_RANGE with *needed set       */
+long pbg_stream_text(pbg_stream *st, uint32_t i, char *out, size_t cap, size_t *needed);
+/* copies the region's packed rows (n_sites * pbg_row_bytes() bytes) into dst, host or device
+ * memory (the statistics' input: lets a caller check a streamed run against a resident one)   */
+int  pbg_stream_rows(const pbg_stream *st, void *dst, size_t cap);
+int  pbg_stream_profile(const pbg_stream *st, pbg_stream_prof *prof);
+void pbg_stream_close(pbg_stream *st);
 
 /* ---- profiling ---------------------------------------------------------------------- */
 /* With timing on, every pbg_call_sites records a pair of HIP events on its stream around its

@@ -27,7 +27,8 @@ PBG_S_TREE = 0x400
 EXPORTS = ["pbg_create", "pbg_destroy", "pbg_last_error", "pbg_row_bytes", "pbg_k_bytes", "pbg_sfs_stride",
            "pbg_device_count", "pbg_call_sites", "pbg_window_stats", "pbg_check", "pbg_run", "pbg_take_text",
            "pbg_format", "pbg_set_kernel_timing", "pbg_kernel_time", "pbg_call_time", "pbg_synth_max_keys",
-           "pbg_synth_pileup"]
+           "pbg_synth_pileup", "pbg_stream_open", "pbg_stream_push", "pbg_stream_finish", "pbg_stream_text",
+           "pbg_stream_rows", "pbg_stream_profile", "pbg_stream_close"]
 
 
 class PbgParams(C.Structure):
@@ -76,6 +77,15 @@ class PbgCmd(C.Structure):
                 ("win_size", C.c_int64), ("beg", C.c_int32), ("end", C.c_int32), ("chr_name", C.c_char_p),
                 ("sample_names", C.POINTER(C.c_char_p)), ("pop_names", C.POINTER(C.c_char_p)),
                 ("refid", C.c_char_p), ("ms_windows", C.c_int32)]
+
+
+class PbgStreamProf(C.Structure):
+    _fields_ = [("h2d_bytes", C.c_uint64), ("pieces", C.c_uint32), ("chunks", C.c_uint32),
+                ("pinned_chunks", C.c_uint32), ("_pad", C.c_uint32), ("ms_stage", C.c_double),
+                ("ms_wait", C.c_double), ("ms_h2d", C.c_double), ("ms_call", C.c_double), ("ms_finish", C.c_double)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "_pad"}
 
 
 _lib = None
@@ -133,6 +143,20 @@ def load():
     lib.pbg_synth_max_keys.restype = C.c_uint64
     lib.pbg_synth_pileup.argtypes = [vp, P(PbgSynthSpec), vp, vp, vp, vp, vp, C.c_uint64, P(C.c_uint64), vp]
     lib.pbg_synth_pileup.restype = C.c_int
+    lib.pbg_stream_open.argtypes = [vp, P(PbgCmd), C.c_uint32, C.c_int32, C.c_uint32, C.c_uint32, P(vp)]
+    lib.pbg_stream_open.restype = C.c_int
+    lib.pbg_stream_push.argtypes = [vp, P(PbgPileup)]
+    lib.pbg_stream_push.restype = C.c_int
+    lib.pbg_stream_finish.argtypes = [vp]
+    lib.pbg_stream_finish.restype = C.c_int
+    lib.pbg_stream_text.argtypes = [vp, C.c_uint32, C.c_char_p, C.c_size_t, P(C.c_size_t)]
+    lib.pbg_stream_text.restype = C.c_long
+    lib.pbg_stream_rows.argtypes = [vp, vp, C.c_size_t]
+    lib.pbg_stream_rows.restype = C.c_int
+    lib.pbg_stream_profile.argtypes = [vp, P(PbgStreamProf)]
+    lib.pbg_stream_profile.restype = C.c_int
+    lib.pbg_stream_close.argtypes = [vp]
+    lib.pbg_stream_close.restype = None
     _lib = lib
     return lib
 
@@ -183,3 +207,51 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+class Stream:
+    """A streamed run (pbg_stream_*): pieces of a region's HOST key batch pushed in position
+    order, then every command's TSV.  `cmds` are PbgCmd structures (kept alive here)."""
+
+    def __init__(self, ctx: Context, cmds, pos0: int, n_sites: int, chunk_sites: int = 0):
+        self.ctx, self.cmds = ctx, list(cmds)
+        arr = (PbgCmd * max(1, len(self.cmds)))(*self.cmds)
+        self._arr = arr
+        self.h = C.c_void_p()
+        ctx.check(ctx.lib.pbg_stream_open(ctx.h, arr, len(self.cmds), pos0, n_sites, chunk_sites, C.byref(self.h)),
+                  "pbg_stream_open")
+
+    def push(self, piece: PbgPileup):
+        self.ctx.check(self.ctx.lib.pbg_stream_push(self.h, C.byref(piece)), "pbg_stream_push")
+
+    def finish(self):
+        self.ctx.check(self.ctx.lib.pbg_stream_finish(self.h), "pbg_stream_finish")
+
+    def text(self, i: int) -> str:
+        need = C.c_size_t(0)
+        r = self.ctx.lib.pbg_stream_text(self.h, i, None, 0, C.byref(need))
+        if r != PBG_E_RANGE:
+            self.ctx.check(r, "pbg_stream_text")
+        buf = C.create_string_buffer(max(1, need.value))
+        self.ctx.check(self.ctx.lib.pbg_stream_text(self.h, i, buf, need.value, C.byref(need)), "pbg_stream_text")
+        return buf.value.decode()
+
+    def rows_into(self, ptr: int, cap: int):
+        """Copy the region's rows into host or device memory at ptr (cap bytes)."""
+        self.ctx.check(self.ctx.lib.pbg_stream_rows(self.h, ptr, cap), "pbg_stream_rows")
+
+    def profile(self) -> dict:
+        pr = PbgStreamProf()
+        self.ctx.check(self.ctx.lib.pbg_stream_profile(self.h, C.byref(pr)), "pbg_stream_profile")
+        return pr.as_dict()
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.pbg_stream_close(self.h)
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

@@ -1,10 +1,6 @@
-// api.cpp -- the C-ABI of include/popbam_gpu.h: context, launches and `pbg_run`.
-//
-// pbg_run restates the window loop of main_<cmd> (e.g. pop_nucdiv.cpp:47-124): windows of
-// `win_size` bases [beg + cw*w, beg + (cw+1)*w - 1) (the last base is dropped, Appendix A.1),
-// num_windows = ((end-beg)-1)/w, or the whole region without -w.  Unlike the reference,
-// which re-fetches and re-piles reads for every window, all positions of the region are
-// called in one launch and every window is reduced in one launch.
+// api.cpp -- the C-ABI of include/popbam_gpu.h: context, resident-batch launches
+// (pbg_call_sites / pbg_window_stats / pbg_check), the synthetic generator and pbg_format.
+// Streamed runs over host batches (pbg_stream_*, pbg_run) are in stream.cpp.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,53 +10,8 @@
 #include <type_traits>
 #include <vector>
 
-#include "pbg_common.h"
-#include "pbg_host.h"
+#include "pbg_ctx.h"
 
-struct pbg_ctx {
-    int device = 0;
-    int n_cu = 256;   // the device's CU count (persistent queue-kernel grid)
-    pbg_params params{};
-    pbg::DevParams dp{};
-    pbg::DevTables dt{};
-    int row_bytes = 8;
-    double *d_fk = nullptr, *d_beta = nullptr, *d_lhet = nullptr, *d_sfs = nullptr, *d_r2 = nullptr;
-    double *d_fbeta = nullptr;
-    double *d_lb = nullptr;
-    double *d_oe = nullptr;
-    int *d_err = nullptr;
-    std::string err;
-    // per-pileup LDS staging capacity (keyed by block_off pointer and size), so repeated
-    // calls on the same resident batch do not synchronise
-    const void *cap_key = nullptr;
-    uint32_t cap_sites = 0, cap_val = 0;
-    // window lists already validated (device pointer, size, rows, statistics), most recent last
-    struct Plan {
-        const void *wins;
-        uint32_t n_win, n_rows, stats;
-        uint64_t zstride;   // ZnS list words per window at fixed places (0: pool)
-    };
-    std::vector<Plan> plans;
-    uint64_t *d_ws = nullptr, *d_wsoff = nullptr, *d_zns = nullptr;
-    size_t zns_cap = 0;   // bytes of d_zns
-    size_t ws_cap = 0, wsoff_cap = 0, segcnt_cap = 0;
-    int32_t *d_segcnt = nullptr;
-    // samples deeper than the register sort width (call kernel): queues + parked info bytes
-    pbg::DeepBufs deep{};
-    size_t deep_sites_cap = 0, deep_info_cap = 0;
-    // pbg_set_kernel_timing: HIP events around the dominant call kernel of every call, and
-    // around the whole call
-    bool timing = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev, evc;
-    size_t ev_used = 0;
-    // pbg_synth_pileup: block-total scan scratch; read-template tables per seed (built once,
-    // never rebuilt while a generator launch on another stream may read them)
-    uint64_t *d_synth = nullptr;
-    size_t synth_cap = 0;
-    std::vector<std::pair<uint64_t, uint16_t *>> tmpl;
-    // pbg_run text kept when the caller's buffer was too small (pbg_take_text)
-    std::string text;
-};
 
 namespace {
 
@@ -71,6 +22,12 @@ int fail(pbg_ctx *c, int code, const std::string &msg) {
     else g_create_error = msg;
     return code;
 }
+
+}  // namespace
+
+int pbg::ctx_fail(pbg_ctx *c, int code, const std::string &msg) { return fail(c, code, msg); }
+
+namespace {
 
 #define HIPCHK(ctx, expr)                                                                          \
     do {                                                                                           \
@@ -108,13 +65,6 @@ hipError_t upload(T **dst, const std::vector<T> &v) {
     return hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
 }
 
-struct DevBuf {   // RAII device allocation for pbg_run
-    void *p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-    hipError_t alloc(size_t bytes) { return hipMalloc(&p, std::max<size_t>(bytes, 16)); }
-};
 
 }  // namespace
 
@@ -299,6 +249,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
 void pbg_destroy(pbg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    pbg::stream_bufs_free(c);
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
                     (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_oe, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, (void *)c->d_zns,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
@@ -318,7 +269,8 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
     if (!c || !pl || !rows) return fail(c, PBG_E_ARG, "null argument");
     if (pl->n_sites == 0) return PBG_OK;
     if (!pl->ref || !pl->k || !pl->rmsq || !pl->block_off || !pl->keys) return fail(c, PBG_E_ARG, "null pileup array");
-    if (((uintptr_t)pl->keys & 15) || ((uintptr_t)rows & 15)) return fail(c, PBG_E_ARG, "keys / rows must be 16-byte aligned");
+    if (((uintptr_t)pl->keys | (uintptr_t)pl->k | (uintptr_t)pl->rmsq | (uintptr_t)rows) & 15)
+        return fail(c, PBG_E_ARG, "keys / k / rmsq / rows must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
     const uint32_t nblk = (pl->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
     if (cb && (c->cap_key != (const void *)pl->block_off || c->cap_sites != pl->n_sites)) {
@@ -387,7 +339,7 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         ++c->ev_used;
         HIPCHK(c, hipEventRecord(c0, (hipStream_t)stream));
     }
-    const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys};
+    const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys, c->d_err};
     HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, B, cap, rows, cb, c->d_err, c->deep,
                                      (hipStream_t)stream, e0, e1, c->n_cu));
     if (c1) HIPCHK(c, hipEventRecord(c1, (hipStream_t)stream));
@@ -403,6 +355,7 @@ int pbg_check(pbg_ctx *c, void *stream) {
     if (!herr) return PBG_OK;
     HIPCHK(c, hipMemset(c->d_err, 0, sizeof(int)));
     if (herr & 4) return fail(c, PBG_E_RANGE, "statistics workspace exhausted (windows with very many segregating sites)");
+    if (herr & 8) return fail(c, PBG_E_BATCH, "a kernel loaded keys outside [block_off[0], block_off[last]) (PBG_BOUNDS build)");
     if (herr & 2) return fail(c, PBG_E_BATCH, "synthetic batch needs more keys than keys_cap");
     return fail(c, PBG_E_BATCH, "pileup block_off disagrees with k[]");
 }
@@ -567,11 +520,21 @@ int pbg_synth_pileup(pbg_ctx *c, const pbg_synth_spec *sp, uint8_t *ref, void *k
     for (auto &t : c->tmpl)
         if (t.first == sp->seed) tmpl = t.second;
     if (!tmpl) {   // first use of this seed: build its table and wait for it (every stream may read it)
+        constexpr size_t kTmplCache = 8;   // tables kept per context (2 MB each)
+        if (c->tmpl.size() >= kTmplCache) {   // evict the oldest once no launch can still read it
+            HIPCHK(c, hipDeviceSynchronize());
+            HIPCHK(c, hipFree(c->tmpl.front().second));
+            c->tmpl.erase(c->tmpl.begin());
+        }
         uint16_t *t = nullptr;
         HIPCHK(c, hipMalloc((void **)&t, pbg::kTmplSize * sizeof(uint16_t)));
-        c->tmpl.emplace_back(sp->seed, t);
-        HIPCHK(c, pbg::launch_synth_tmpl(sp->seed, t, s));
-        HIPCHK(c, hipStreamSynchronize(s));
+        hipError_t e = pbg::launch_synth_tmpl(sp->seed, t, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {   // never cache a table that was not built
+            (void)hipFree(t);
+            return fail(c, PBG_E_HIP, std::string("synthetic template table: ") + hipGetErrorString(e));
+        }
+        c->tmpl.emplace_back(sp->seed, t);   // cached only once built
         tmpl = t;
     }
     const size_t need = pbg::synth_scratch_words(sp->n_sites) * 8;
@@ -590,276 +553,6 @@ int pbg_synth_pileup(pbg_ctx *c, const pbg_synth_spec *sp, uint8_t *ref, void *k
         if (rc) return rc;
     }
     return PBG_OK;
-}
-
-long pbg_run(pbg_ctx *c, const pbg_cmd *cmd, const pbg_pileup *hp, char *out, size_t cap, size_t *needed) {
-    if (!c || !cmd || !hp || (!out && cap)) return fail(c, PBG_E_ARG, "null argument");
-    if (hp->n_sites && (!hp->ref || !hp->k || !hp->rmsq || !hp->keys)) return fail(c, PBG_E_ARG, "null pileup array");
-    HIPCHK(c, hipSetDevice(c->device));
-    c->text.clear();
-    c->cap_key = nullptr;   // this call's buffers are fresh allocations: drop cached plans
-    c->plans.clear();
-    const int n = c->dp.n, np = c->dp.npops;
-    // ---- windows in contig coordinates (main_<cmd>)
-    std::vector<std::pair<int32_t, int32_t>> win;
-    if (cmd->windowed) {
-        const int64_t w = cmd->win_size;
-        if (w <= 0) return fail(c, PBG_E_ARG, "window size must be positive");
-        const int64_t nw = ((int64_t)(cmd->end - cmd->beg) - 1) / w;
-        for (int64_t cw = 0; cw < nw; ++cw)
-            win.emplace_back((int32_t)(cmd->beg + cw * w), (int32_t)((cw + 1) * w + (cmd->beg - 1)));
-    } else {
-        win.emplace_back(cmd->beg, cmd->end);
-    }
-    // ---- the 64-position blocks of the batch the windows touch
-    const int64_t pos0 = hp->pos0, pend = (int64_t)hp->pos0 + hp->n_sites;
-    int64_t lo = pend, hi = pos0;
-    for (auto &x : win) {
-        int64_t a = std::max<int64_t>(x.first, pos0), b = std::min<int64_t>(x.second, pend);
-        if (a < b) {
-            lo = std::min(lo, a);
-            hi = std::max(hi, b);
-        }
-    }
-    std::vector<uint64_t> boff;
-    const uint64_t *hboff = hp->block_off;
-    const int kb = c->dp.k16 ? 2 : 1;
-    const uint32_t nblk_all = (hp->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
-    if (!hboff) {
-        boff.assign(nblk_all + 1, 0);
-        uint64_t run = 0;
-        for (uint32_t b = 0; b < nblk_all; ++b) {
-            boff[b] = run;
-            const uint32_t s1 = std::min<uint32_t>(hp->n_sites, (b + 1) * pbg::kSiteBlock);
-            for (size_t i = (size_t)b * pbg::kSiteBlock * n; i < (size_t)s1 * n; ++i)
-                run += kb == 1 ? ((const uint8_t *)hp->k)[i] : ((const uint16_t *)hp->k)[i];
-        }
-        boff[nblk_all] = run;
-        hboff = boff.data();
-    }
-    uint32_t blo = 0, bhi = 0;
-    if (lo < hi) {
-        blo = (uint32_t)((lo - pos0) / pbg::kSiteBlock);
-        bhi = (uint32_t)((hi - pos0 + pbg::kSiteBlock - 1) / pbg::kSiteBlock);
-    }
-    const uint32_t dsites = lo < hi ? std::min<uint32_t>(hp->n_sites, bhi * pbg::kSiteBlock) - blo * pbg::kSiteBlock : 0;
-    const int64_t dpos0 = pos0 + (int64_t)blo * pbg::kSiteBlock;
-    const uint64_t r0 = lo < hi ? hboff[blo] : 0, r1 = lo < hi ? hboff[bhi] : 0;
-    const uint32_t dblk = bhi - blo;
-
-    DevBuf d_ref, d_k, d_rq, d_boff, d_keys, d_rows, d_cb, d_win;
-    hipStream_t s = nullptr;
-    const int rb = c->row_bytes;
-    const bool is_snp = cmd->cmd == PBG_CMD_SNP;
-    const bool snp_words = is_snp && cmd->output == 0;   // only -o 0 prints consensus words
-    if (dsites) {
-        std::vector<uint64_t> lb(dblk + 1);
-        for (uint32_t b = 0; b <= dblk; ++b) lb[b] = hboff[blo + b] - r0;
-        const size_t t0 = (size_t)blo * pbg::kSiteBlock * n, nt = (size_t)dsites * n;
-        HIPCHK(c, d_ref.alloc(dsites));
-        HIPCHK(c, d_k.alloc(nt * kb));
-        HIPCHK(c, d_rq.alloc(nt * 4));
-        HIPCHK(c, d_boff.alloc((dblk + 1) * 8));
-        HIPCHK(c, d_keys.alloc((r1 - r0) * 2));
-        HIPCHK(c, d_rows.alloc(((size_t)dsites * rb + 15) & ~(size_t)15));
-        HIPCHK(c, hipMemcpy(d_ref.p, hp->ref + (size_t)blo * pbg::kSiteBlock, dsites, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(d_k.p, (const char *)hp->k + t0 * kb, nt * kb, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(d_rq.p, hp->rmsq + t0, nt * 4, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(d_boff.p, lb.data(), (dblk + 1) * 8, hipMemcpyHostToDevice));
-        if (r1 > r0) HIPCHK(c, hipMemcpy(d_keys.p, hp->keys + r0, (r1 - r0) * 2, hipMemcpyHostToDevice));
-        if (snp_words) HIPCHK(c, d_cb.alloc((size_t)dsites * n * 8));
-        pbg_pileup dp{dsites, (int32_t)dpos0, (const uint8_t *)d_ref.p, d_k.p, (const uint32_t *)d_rq.p,
-                      (const uint64_t *)d_boff.p, (const uint16_t *)d_keys.p};
-        int rc = pbg_call_sites(c, &dp, d_rows.p, snp_words ? (uint64_t *)d_cb.p : nullptr, s);
-        if (rc) return rc;
-        if ((rc = pbg_check(c, s))) return rc;
-    }
-    std::string text;
-    if (is_snp) {
-        // print_snp per window (pop_snp.cpp:218-317): segregating positions in order, as
-        // print_popbam_snp (-o 0), print_sweep (-o 1) or print_ms (-o 2, header first)
-        if (cmd->output < 0 || cmd->output > 2) return fail(c, PBG_E_ARG, "snp output format must be 0, 1 or 2");
-        std::vector<unsigned char> rows((size_t)dsites * rb);
-        std::vector<uint64_t> cb(snp_words ? (size_t)dsites * n : 0);
-        if (dsites) {
-            HIPCHK(c, hipMemcpy(rows.data(), d_rows.p, rows.size(), hipMemcpyDeviceToHost));
-            if (snp_words) HIPCHK(c, hipMemcpy(cb.data(), d_cb.p, cb.size() * 8, hipMemcpyDeviceToHost));
-        }
-        using pbg::mask128;
-        const mask128 tmask = ((mask128)1 << n) - 1;   // n <= 126
-        std::vector<mask128> pmask(np);
-        for (int i = 0; i < np; ++i) pmask[i] = ((mask128)c->dp.pop_mask_hi[i] << 64) | c->dp.pop_mask[i];
-        // print_ms prints its header in the window loop at cw == 0 (pop_snp.cpp:114-115): not at
-        // all without windows; a block of a longer run passes the run's count or suppresses it
-        if (cmd->output == 2 && cmd->ms_windows >= 0 && !win.empty())
-            pbg::format_ms_header(text, n, np, c->params.pop_n, cmd->ms_windows > 0 ? (long)cmd->ms_windows : (long)win.size());
-        std::vector<int32_t> wpos;
-        std::vector<mask128> wtypes;
-        for (auto &x : win) {
-            wpos.clear();
-            wtypes.clear();
-            for (int64_t p = std::max<int64_t>(x.first, dpos0); p < std::min<int64_t>(x.second, dpos0 + dsites); ++p) {
-                const size_t i = (size_t)(p - dpos0);
-                const unsigned char *r = rows.data() + i * rb;
-                if (!((r[rb - 1] >> 7) & 1)) continue;   // not segregating
-                mask128 types = 0;
-                for (int b = 0; b < rb; ++b) types |= (mask128)r[b] << (8 * b);
-                types &= tmask;
-                if (cmd->output == 0)
-                    pbg::format_snp_site(text, *cmd, n, (int32_t)p, hp->ref[p - pos0] & 0x7f, cb.data() + i * n);
-                else if (cmd->output == 1)
-                    pbg::format_sweep_site(text, *cmd, np, pmask.data(), c->params.flag, (int32_t)p, types);
-                wpos.push_back((int32_t)p);
-                wtypes.push_back(types);
-            }
-            if (cmd->output == 2) pbg::format_ms_window(text, n, c->params.flag, cmd->outidx, x.first, x.second, wpos, wtypes);
-        }
-    } else {
-        uint32_t stats = 0;
-        switch (cmd->cmd) {
-            case PBG_CMD_NUCDIV: stats = PBG_S_NUCDIV; break;
-            case PBG_CMD_SFS: stats = PBG_S_SFS; break;
-            case PBG_CMD_LD: stats = cmd->output == 1 ? PBG_S_OMEGA : cmd->output == 2 ? PBG_S_WALL : PBG_S_ZNS; break;
-            case PBG_CMD_DIVERGE: stats = cmd->output == 1 ? PBG_S_DIV_POP : PBG_S_DIV_IND; break;
-            case PBG_CMD_HAPLO:
-                stats = cmd->output == 1 ? PBG_S_HAP_EHHS : cmd->output == 2 ? PBG_S_HAP_DXY : PBG_S_HAP_K;
-                break;
-            case PBG_CMD_TREE:
-                // join_tree's last cycle needs three clusters (ntaxa = n + 1 >= 3)
-                if (n < 2) return fail(c, PBG_E_ARG, "tree needs at least two samples");
-                stats = PBG_S_TREE;
-                break;
-            default: return fail(c, PBG_E_ARG, "unsupported subcommand");
-        }
-        const uint32_t nw = (uint32_t)win.size();
-        // row ranges: clip each window to the uploaded rows (positions outside have no callback)
-        std::vector<pbg_window> rw(nw);
-        for (uint32_t i = 0; i < nw; ++i) {
-            int64_t a = std::min<int64_t>(std::max<int64_t>(win[i].first, dpos0), dpos0 + dsites);
-            int64_t b = std::min<int64_t>(std::max<int64_t>(win[i].second, a), dpos0 + dsites);
-            rw[i].beg = (int32_t)(a - dpos0);
-            rw[i].end = (int32_t)(b - dpos0);
-        }
-        const int npairs = std::max(1, np * (np - 1));
-        const size_t szw = nw, szp = (size_t)nw * np, szq = (size_t)nw * npairs, szn = (size_t)nw * n;
-        const size_t szt = stats == PBG_S_TREE ? (size_t)nw * (n + 1) * (n + 1) : 1;
-        DevBuf o_ns, o_seg, o_d1, o_d2, o_d3, o_i1, o_i2, o_i3, o_td, o_bins;
-        const bool theta = stats == PBG_S_SFS && (cmd->output & 1);   // sfs --theta
-        const size_t szb = theta ? szp * (size_t)c->dp.sfs_stride : 1;
-        HIPCHK(c, d_win.alloc(nw * sizeof(pbg_window)));
-        HIPCHK(c, hipMemcpy(d_win.p, rw.data(), nw * sizeof(pbg_window), hipMemcpyHostToDevice));
-        HIPCHK(c, o_ns.alloc(szw * 4));
-        HIPCHK(c, o_seg.alloc(szw * 4));
-        HIPCHK(c, o_d1.alloc(std::max(szq, std::max(szp, szn)) * 8));
-        HIPCHK(c, o_d2.alloc(std::max(szq, szp) * 8));
-        HIPCHK(c, o_d3.alloc(szp * 8));
-        HIPCHK(c, o_i1.alloc(szp * 4));
-        HIPCHK(c, o_i2.alloc(szp * 4));
-        HIPCHK(c, o_i3.alloc(szq * 4));
-        HIPCHK(c, o_td.alloc(szt * 4));
-        HIPCHK(c, o_bins.alloc(szb * 4));
-        pbg_window_out O{};
-        O.num_sites = (int32_t *)o_ns.p;
-        O.segsites = (int32_t *)o_seg.p;
-        double *d1 = (double *)o_d1.p, *d2 = (double *)o_d2.p, *d3 = (double *)o_d3.p;
-        int32_t *i1 = (int32_t *)o_i1.p, *i2 = (int32_t *)o_i2.p, *i3 = (int32_t *)o_i3.p;
-        switch (stats) {
-            case PBG_S_NUCDIV: O.pi = d1; O.dxy = d2; break;
-            case PBG_S_SFS:
-                O.td = d1; O.fwh = d2;
-                if (theta) { O.seg_pop = i1; O.theta_w = d3; O.sfs_bins = (int32_t *)o_bins.p; }
-                break;
-            case PBG_S_ZNS: case PBG_S_OMEGA: O.ld_snps = i1; O.ld_val = d1; break;
-            case PBG_S_WALL: O.ld_snps = i1; O.ld_val = d1; O.ld_q = d2; break;
-            case PBG_S_DIV_IND: O.div_ind = d1; break;
-            case PBG_S_DIV_POP: O.div_fixed = i1; O.div_seg = i2; O.div_pop = d1; break;
-            case PBG_S_HAP_K: O.nhaps = i1; O.hap_val = d1; break;
-            case PBG_S_HAP_EHHS: O.hap_val = d1; break;
-            case PBG_S_HAP_DXY: O.hap_val = d3; O.hap_dxy = d1; O.hap_min = i3; break;
-            case PBG_S_TREE: O.tree_diff = (int32_t *)o_td.p; break;
-        }
-        pbg_stat_opts so{stats, cmd->min_freq, cmd->outidx, cmd->jc};
-        // an all-empty batch still needs one addressable row for the kernel's pointer
-        DevBuf dummy;
-        const void *rows_p = d_rows.p;
-        if (!rows_p) {
-            HIPCHK(c, dummy.alloc(16));
-            HIPCHK(c, hipMemset(dummy.p, 0, 16));
-            rows_p = dummy.p;
-        }
-        int rc = pbg_window_stats(c, rows_p, dsites, (const pbg_window *)d_win.p, nw, &so, &O, s);
-        if (rc) return rc;
-        if ((rc = pbg_check(c, s))) return rc;
-        std::vector<int32_t> h_ns(szw), h_seg(szw), h_i1(szp), h_i2(szp), h_i3(szq), h_td(szt);
-        std::vector<double> h_d1(std::max(szq, std::max(szp, szn))), h_d2(std::max(szq, szp)), h_d3(szp);
-        HIPCHK(c, hipMemcpy(h_ns.data(), o_ns.p, szw * 4, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(h_seg.data(), o_seg.p, szw * 4, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(h_i1.data(), o_i1.p, szp * 4, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(h_i2.data(), o_i2.p, szp * 4, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(h_i3.data(), o_i3.p, szq * 4, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(h_td.data(), o_td.p, szt * 4, hipMemcpyDeviceToHost));
-        std::vector<int32_t> h_bins(szb);
-        HIPCHK(c, hipMemcpy(h_bins.data(), o_bins.p, szb * 4, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(h_d1.data(), o_d1.p, h_d1.size() * 8, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(h_d2.data(), o_d2.p, h_d2.size() * 8, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(h_d3.data(), o_d3.p, h_d3.size() * 8, hipMemcpyDeviceToHost));
-        pbg::WindowHost wh;
-        for (uint32_t i = 0; i < nw; ++i) {
-            wh.beg = win[i].first;
-            wh.end = win[i].second;
-            wh.num_sites = h_ns[i];
-            wh.segsites = h_seg[i];
-            auto slice = [](const auto &v, size_t off, size_t cnt) {
-                using T = typename std::decay_t<decltype(v)>::value_type;
-                return std::vector<T>(v.begin() + off, v.begin() + off + cnt);
-            };
-            switch (stats) {
-                case PBG_S_NUCDIV: wh.pi = slice(h_d1, i * np, np); wh.dxy = slice(h_d2, i * npairs, npairs); break;
-                case PBG_S_SFS:
-                    wh.td = slice(h_d1, i * np, np); wh.fwh = slice(h_d2, i * np, np);
-                    if (theta) {
-                        wh.seg_pop = slice(h_i1, i * np, np); wh.theta_w = slice(h_d3, i * np, np);
-                        wh.sfs_bins.assign(np, {});
-                        for (int p = 0; p < np; ++p)
-                            wh.sfs_bins[p] = slice(h_bins, ((size_t)i * np + p) * c->dp.sfs_stride,
-                                                   (size_t)c->dp.pop_n[p] + 1);
-                    }
-                    break;
-                case PBG_S_ZNS: case PBG_S_OMEGA:
-                    wh.ld_snps = slice(h_i1, i * np, np); wh.ld_val = slice(h_d1, i * np, np); break;
-                case PBG_S_WALL:
-                    wh.ld_snps = slice(h_i1, i * np, np); wh.ld_val = slice(h_d1, i * np, np);
-                    wh.ld_q = slice(h_d2, i * np, np); break;
-                case PBG_S_DIV_IND: wh.div_ind = slice(h_d1, i * n, n); break;
-                case PBG_S_DIV_POP:
-                    wh.div_fixed = slice(h_i1, i * np, np); wh.div_seg = slice(h_i2, i * np, np);
-                    wh.div_pop = slice(h_d1, i * np, np); break;
-                case PBG_S_HAP_K: wh.nhaps = slice(h_i1, i * np, np); wh.hap_val = slice(h_d1, i * np, np); break;
-                case PBG_S_HAP_EHHS: wh.hap_val = slice(h_d1, i * np, np); break;
-                case PBG_S_HAP_DXY:
-                    wh.hap_val = slice(h_d3, i * np, np); wh.hap_dxy = slice(h_d1, i * npairs, npairs);
-                    wh.hap_min = slice(h_i3, i * npairs, npairs); break;
-                case PBG_S_TREE: wh.tree_diff = slice(h_td, i * (n + 1) * (n + 1), (size_t)(n + 1) * (n + 1)); break;
-            }
-            pbg::format_window(text, *cmd, n, np, c->dp.flag, wh);
-        }
-    }
-    if (needed) *needed = text.size() + 1;
-    if (text.size() + 1 > cap) {
-        c->text.swap(text);   // kept for pbg_take_text
-        return fail(c, PBG_E_RANGE, "output buffer too small");
-    }
-    std::memcpy(out, text.c_str(), text.size() + 1);
-    return (long)text.size();
-}
-
-long pbg_take_text(pbg_ctx *c, char *out, size_t cap) {
-    if (!c || (!out && cap)) return fail(c, PBG_E_ARG, "null argument");
-    if (c->text.size() + 1 > cap) return fail(c, PBG_E_RANGE, "output buffer too small");
-    std::memcpy(out, c->text.c_str(), c->text.size() + 1);
-    const long len = (long)c->text.size();
-    std::string().swap(c->text);
-    return len;
 }
 
 long pbg_format(const pbg_ctx *c, const pbg_cmd *cmd, const pbg_window_out *ho, uint32_t n_win, const int32_t *wbeg,

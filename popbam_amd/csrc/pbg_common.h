@@ -254,7 +254,30 @@ struct Batch {
     const uint32_t *rmsq;
     const uint64_t *block_off;
     const uint16_t *keys;
+    int *err;                      // the context's error word (PBG_BOUNDS checks)
 };
+
+// PBG_BOUNDS debug build (make bounds -> popbam_amd/variants/bounds/libpopbam_gpu.so): every key
+// load of the call kernels is checked against the contract of include/popbam_gpu.h -- keys are
+// read only from the 16-byte chunks of keys[] that hold keys [block_off[0], block_off[last]) --
+// and a load outside sets err bit 8 (pbg_check: PBG_E_BATCH).  The product build compiles the
+// checks away.
+#ifdef PBG_BOUNDS
+__device__ __forceinline__ void bounds_range(const Batch &B, uint64_t lo, uint64_t n) {   // key indices [lo, lo + n)
+    if (n == 0) return;
+    const uint32_t nblk = (B.n_sites + kSiteBlock - 1) / kSiteBlock;
+    if (lo < B.block_off[0] || lo + n > B.block_off[nblk]) atomicOr(B.err, 8);
+}
+__device__ __forceinline__ void bounds_chunk(const Batch &B, uint64_t c) {   // 16-byte chunk c of keys[]
+    const uint32_t nblk = (B.n_sites + kSiteBlock - 1) / kSiteBlock;
+    if (8 * c + 8 <= B.block_off[0] || 8 * c >= B.block_off[nblk]) atomicOr(B.err, 8);
+}
+#define PBG_BOUNDS_KEYS(B, lo, n) ::pbg::bounds_range((B), (lo), (n))
+#define PBG_BOUNDS_CHUNK(B, c) ::pbg::bounds_chunk((B), (c))
+#else
+#define PBG_BOUNDS_KEYS(B, lo, n) ((void)0)
+#define PBG_BOUNDS_CHUNK(B, c) ((void)0)
+#endif
 
 // kernel launchers (defined in call_kernel.hip / stats_kernel.hip)
 // n_cu: the context device's CU count (sizes the persistent queue kernel's grid).

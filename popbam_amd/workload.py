@@ -275,9 +275,6 @@ class HotPath:
                 self.ctx.check(self.ctx.lib.pbg_window_stats(self.ctx.h, rows, nrows, _ptr(w), nw, C.byref(self.opts),
                                                              C.byref(o), stream.cuda_stream), "pbg_window_stats")
 
-    def host_stream(self, host: dict, chunk_sites: int, window: int) -> "HostStream":
-        return HostStream(self, host, chunk_sites, window)
-
     def step_pipelined(self, call_stream, stats_stream):
         """call(piece i) on call_stream; stats(piece i) on stats_stream after it.  The statistics
         of piece i run beside the call of piece i+1, and the last piece's beside the next step's
@@ -302,94 +299,3 @@ class HotPath:
                 self.ctx.check(lib.pbg_window_stats(h, rows, nrows, _ptr(w), nw, C.byref(self.opts), C.byref(o),
                                                     stats_stream.cuda_stream), "pbg_window_stats")
         call_stream.wait_stream(stats_stream)
-
-
-class HostStream:
-    """The hot path fed from HOST memory (the drop-in boundary hands over a pinned key batch):
-    the contig in chunks of whole windows, each chunk's ref / k / rmsq / block_off / keys copied
-    host -> device on a copy stream into one of two device slots while the previous chunk is
-    called and its windows computed on the compute stream (double buffering).  Rows and window
-    outputs land in the HotPath's full-size arrays, so a pass is checkable against the resident
-    path.  block_off keeps the host batch's absolute key offsets: the keys pointer handed to
-    pbg_call_sites is the slot's buffer shifted back by the chunk's first (16-byte aligned) key."""
-
-    def __init__(self, hp: HotPath, host: dict, chunk_sites: int, window: int, device: str = "cuda"):
-        import math
-        self.hp, self.host = hp, host
-        ctx = hp.ctx
-        n, kb = ctx.params.n_samples, ctx.k_bytes
-        unit = SITE_BLOCK * window // math.gcd(SITE_BLOCK, window)
-        chunk = max(unit, chunk_sites // unit * unit)
-        ns = hp.synth.n_sites
-        self.bounds = [(a, min(ns, a + chunk)) for a in range(0, ns, chunk)]
-        boff = host["block_off"]
-        plans = {}
-        self.chunks = []
-        max_keys = 0
-        for p0, p1 in self.bounds:
-            b0, b1 = p0 // SITE_BLOCK, (p1 + SITE_BLOCK - 1) // SITE_BLOCK
-            ka, kz = int(boff[b0]) & ~7, int(boff[b1])
-            max_keys = max(max_keys, kz - ka)
-            idx = [i for i, (b, e) in enumerate(hp.windows) if b >= p0 and e <= p1]
-            rel = tuple((hp.windows[i][0] - p0, hp.windows[i][1] - p0) for i in idx)
-            if rel not in plans:   # one device window list per distinct shape (pbg_window_stats caches its plan)
-                plans[rel] = torch.tensor([x for ab in rel for x in ab] or [0, 0], dtype=torch.int32).to(device)
-            self.chunks.append((p0, p1, b0, b1, ka, kz, idx, plans[rel]))
-        assert sum(len(c[6]) for c in self.chunks) == hp.n_win, "a window spans a chunk border"
-        self.chunk = chunk
-        csz = chunk
-        nb = (csz + SITE_BLOCK - 1) // SITE_BLOCK
-        self.slots = [{"ref": torch.empty(csz, dtype=torch.uint8, device=device),
-                       "k": torch.empty(csz * n, dtype=hp.synth.k.dtype, device=device),
-                       "rmsq": torch.empty(csz * n, dtype=torch.int32, device=device),
-                       "block_off": torch.empty(nb + 1, dtype=torch.int64, device=device),
-                       "keys": torch.empty(max(8, max_keys + 8), dtype=torch.int16, device=device)} for _ in range(2)]
-        self.kb = kb
-        self.copy_stream = torch.cuda.Stream()
-        self.ev_in = [torch.cuda.Event() for _ in range(2)]
-        self.ev_free = [torch.cuda.Event() for _ in range(2)]
-        self.used = [False, False]
-        per_win = {k: (t.numel() // max(1, hp.n_win), t.element_size()) for k, t in hp.out.t.items()}
-        self.outs = []
-        for p0, p1, b0, b1, ka, kz, idx, w in self.chunks:
-            o = _lib.PbgWindowOut()
-            w0 = idx[0] if idx else 0
-            for k in hp.fields_for(hp.stats):
-                per, es = per_win[k]
-                setattr(o, k, _ptr(hp.out.t[k]) + w0 * per * es)
-            self.outs.append(o)
-        self.h2d_bytes = sum(self.chunk_bytes(c) for c in range(len(self.chunks)))
-
-    def chunk_bytes(self, c: int) -> int:
-        p0, p1, b0, b1, ka, kz, _, _ = self.chunks[c]
-        n = self.hp.ctx.params.n_samples
-        return (p1 - p0) * (1 + n * (self.kb + 4)) + 8 * (b1 - b0 + 1) + 2 * (kz - ka)
-
-    def run(self, compute=None):
-        """One pass over the contig; returns after enqueueing (the caller synchronises)."""
-        hp, h = self.hp, self.host
-        ctx, lib = hp.ctx, hp.ctx.lib
-        n = ctx.params.n_samples
-        compute = compute or torch.cuda.current_stream()
-        for c, (p0, p1, b0, b1, ka, kz, idx, w) in enumerate(self.chunks):
-            s = c & 1
-            sl = self.slots[s]
-            if self.used[s]:
-                self.copy_stream.wait_event(self.ev_free[s])   # the slot's previous call + stats are done
-            with torch.cuda.stream(self.copy_stream):
-                sl["ref"][:p1 - p0].copy_(h["ref"][p0:p1], non_blocking=True)
-                sl["k"][:(p1 - p0) * n].copy_(h["k"][p0 * n:p1 * n], non_blocking=True)
-                sl["rmsq"][:(p1 - p0) * n].copy_(h["rmsq"][p0 * n:p1 * n], non_blocking=True)
-                sl["block_off"][:b1 - b0 + 1].copy_(h["block_off"][b0:b1 + 1], non_blocking=True)
-                sl["keys"][:kz - ka].copy_(h["keys"][ka:kz], non_blocking=True)
-            self.ev_in[s].record(self.copy_stream)
-            compute.wait_event(self.ev_in[s])
-            pl = _lib.PbgPileup(p1 - p0, hp.synth.pos0 + p0, _ptr(sl["ref"]), _ptr(sl["k"]), _ptr(sl["rmsq"]),
-                                _ptr(sl["block_off"]), _ptr(sl["keys"]) - 2 * ka)
-            rows = _ptr(hp.rows) + p0 * ctx.row_bytes
-            ctx.check(lib.pbg_call_sites(ctx.h, C.byref(pl), rows, None, compute.cuda_stream), "pbg_call_sites")
-            if idx:
-                ctx.check(lib.pbg_window_stats(ctx.h, rows, p1 - p0, _ptr(w), len(idx), C.byref(hp.opts),
-                                               C.byref(self.outs[c]), compute.cuda_stream), "pbg_window_stats")
-            self.ev_free[s].record(compute)
-            self.used[s] = True

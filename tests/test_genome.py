@@ -71,6 +71,35 @@ def test_chunked_pass_equals_one_batch(gpu_lib, n, npops):
     ctx.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,config", [(24, 3), (96, 4)])
+def test_serial_pass_equals_double_buffered(gpu_lib, n, config):
+    """GenomePass(serial=True) -- each chunk generated on the call stream right before its call,
+    one buffer: the mode bench.py times by default -- writes the same rows, window outputs and
+    key_total as the double-buffered pass, over two passes."""
+    from popbam_amd import _lib
+    ctx = _lib.Context(workload.default_params(n, 2), 0)
+    if config == 3:
+        segs = [genome.Segment(0, 0, 700_001), genome.Segment(2, 100_000, 400_017)]
+        stats, win = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS | _lib.PBG_S_DIV_IND, 10_000
+    else:
+        segs = genome.plan_overlapping(300_000, 1, 1000, 500)[0]
+        stats, win = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_HAP_EHHS, 1000
+    got = []
+    for serial in (True, False):
+        gp = genome.GenomePass(ctx, segs, SEED + n, 10, win, stats, chunk=64 * 1500, serial=serial)
+        for _ in range(2):
+            gp.run()
+        gp.synchronize()
+        got.append((gp.rows.cpu().numpy(), {f: gp.window_results(f) for f in workload.HotPath.fields_for(stats)},
+                    int(gp.key_total.item())))
+    assert np.array_equal(got[0][0], got[1][0])
+    for f in got[0][1]:
+        assert np.array_equal(got[0][1][f].view(np.uint8), got[1][1][f].view(np.uint8)), f
+    assert got[0][2] == got[1][2] > 0
+    ctx.close()
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 8, 13])
 @pytest.mark.parametrize("length,win,step", [(200_000_000, 1000, 500), (10_007, 1000, 500), (5_000, 700, 300),
                                              (999, 1000, 500)])

@@ -341,19 +341,36 @@ def test_sfs_bins_and_theta_w(gpu_lib, n, npops, flag, outidx):
     ctx.close()
 
 
-def test_inconsistent_batch_is_reported(gpu_lib):
-    """pbg_call_sites on a batch whose block_off disagrees with k[]: the kernels never read past
-    the block's keys, write uncounted rows, and pbg_check reports PBG_E_BATCH (then clears)."""
+@pytest.mark.parametrize("n", [12, 32, 96])
+@pytest.mark.parametrize("max_depth", [255, 300])
+def test_inconsistent_batch_is_reported(gpu_lib, n, max_depth):
+    """pbg_call_sites on a batch whose block_off disagrees with k[] for two blocks (4 and 5):
+    the kernels never read past a block's keys, write uncounted rows for exactly those blocks,
+    every other block's rows are byte-identical to the clean batch's, and pbg_check reports
+    PBG_E_BATCH (then clears).  n = 12 keeps the scan's info bytes in LDS (k sum checked after
+    the rounds); 32 and 96 take the wide path (k sum checked before the rounds, mid-block list
+    passes); max_depth 300 stores k as u16."""
     import torch
     from popbam_amd import _lib, workload
-    ctx, params = _ctx(12)
-    syn = workload.SynthPileup(ctx, 64 * 100, 10, SEED)
-    syn.block_off[5] += 3
-    hp = workload.HotPath(ctx, syn, [(0, 64 * 100)], 0)
-    for cb in (None, torch.zeros(64 * 100 * 12, dtype=torch.int64, device="cuda")):
+    ctx, params = _ctx(n, max_depth=max_depth)
+    L = 64 * 100
+    syn = workload.SynthPileup(ctx, L, 10, SEED + n)
+    rb = ctx.row_bytes
+    for cb in (None, torch.zeros(L * n, dtype=torch.int64, device="cuda")):
+        hp = workload.HotPath(ctx, syn, [(0, L)], 0)
+        hp.call(cb=cb)
+        assert ctx.lib.pbg_check(ctx.h, None) == _lib.PBG_OK
+        good = hp.rows.cpu().numpy().reshape(L, rb).copy()
+        syn.block_off[5] += 3
+        hp.rows.fill_(0xAB)
         hp.call(cb=cb)
         assert ctx.lib.pbg_check(ctx.h, None) == _lib.PBG_E_BATCH
         assert ctx.lib.pbg_check(ctx.h, None) == _lib.PBG_OK
+        bad = hp.rows.cpu().numpy().reshape(L, rb)
+        assert not bad[4 * 64:6 * 64].any(), "the corrupted blocks' rows must be uncounted (0)"
+        assert np.array_equal(bad[:4 * 64], good[:4 * 64]) and np.array_equal(bad[6 * 64:], good[6 * 64:])
+        assert good[4 * 64:6 * 64].any()
+        syn.block_off[5] -= 3
     ctx.close()
 
 
@@ -387,15 +404,19 @@ def test_pipelined_pieces_equal_one_step(gpu_lib, n, npops, pieces):
     ctx.close()
 
 
-@pytest.mark.parametrize("n,npops", [(12, 2), (32, 2)])
-def test_host_stream_equals_resident(gpu_lib, n, npops):
-    """The host-input pipeline (workload.HostStream: pinned host batch -> H2D into two device
-    slots per chunk of whole windows, keys pointer shifted back so block_off stays absolute,
-    pbg_call_sites + pbg_window_stats per chunk) writes the same rows and window outputs as one
-    HBM-resident step.  The kernels must read only keys [block_off[0], block_off[last]) of the
-    shifted pointer (include/popbam_gpu.h)."""
+@pytest.mark.parametrize("n,npops,pinned,chunk", [(12, 2, True, 64 * 2000), (12, 2, False, 64 * 3000),
+                                                  (32, 2, True, 0), (96, 3, False, 64 * 700)])
+def test_stream_equals_resident(gpu_lib, n, npops, pinned, chunk):
+    """The C-ABI streamed run (pbg_stream_open / _push / _finish): the batch handed over in HOST
+    memory -- pinned (DMA straight from the caller's buffers) or pageable (threaded copy into the
+    context's pinned staging) -- in several pieces, each split into device chunks that alternate
+    between two slots, gives the resident step's rows bit for bit and its nucdiv / sfs / ld text
+    byte for byte, twice in a row on the same context (slots, window lists and plans reused).
+    The keys pointer of each chunk is shifted back to the chunk's first key, so the kernels must
+    read only keys [block_off[0], block_off[last]) (include/popbam_gpu.h)."""
     import torch
     from popbam_amd import _lib, workload
+    import bench
     stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS | _lib.PBG_S_ZNS
     ctx, params = _ctx(n, npops)
     n_sites = 1_000_000 + 37
@@ -404,19 +425,30 @@ def test_host_stream_equals_resident(gpu_lib, n, npops):
     hp = workload.HotPath(ctx, syn, wins, stats)
     hp.step()
     ctx.sync_check()
-    want_rows = hp.rows.clone()
-    fields = workload.HotPath.fields_for(stats)
-    want = {k: hp.out.t[k].clone() for k in fields}
-    hs = hp.host_stream(hp.to_host(), 240_000, 10_000)
-    assert len(hs.chunks) >= 4
-    hp.rows.zero_()
-    for k in fields:
-        hp.out.t[k].zero_()
-    for _ in range(2):   # the second pass reuses both slots
-        hs.run(torch.cuda.current_stream())
-    torch.cuda.synchronize()
-    ctx.sync_check()
-    assert torch.equal(hp.rows, want_rows)
-    for k in fields:
-        assert torch.equal(hp.out.t[k].view(torch.uint8), want[k].view(torch.uint8)), k
+
+    class A:
+        window = 10_000
+    cmds, keep = bench.stat_cmds(A, n, npops, 0, n_sites)
+    want = bench.resident_texts(ctx, hp, cmds, wins)
+    host = hp.to_host()
+    if not pinned:
+        host = {k: v.clone() for k, v in host.items()}   # pageable copies
+        assert not host["keys"].is_pinned()
+    kb = ctx.k_bytes
+    cuts = [0, 64 * 3001, 64 * 9000, n_sites]   # three pieces: multiples of 64 but the last
+    for _ in range(2):
+        with _lib.Stream(ctx, cmds, 0, n_sites, chunk) as st:
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                pl = _lib.PbgPileup(b - a, a, host["ref"].data_ptr() + a, host["k"].data_ptr() + a * n * kb,
+                                    host["rmsq"].data_ptr() + a * n * 4, host["block_off"].data_ptr() + (a // 64) * 8,
+                                    host["keys"].data_ptr())
+                st.push(pl)
+            st.finish()
+            rows = torch.zeros_like(hp.rows)
+            st.rows_into(rows.data_ptr(), rows.numel())
+            assert torch.equal(rows, hp.rows)
+            assert [st.text(i) for i in range(3)] == want
+            prof = st.profile()
+            assert prof["pieces"] == 3 and prof["chunks"] >= 3
+            assert (prof["pinned_chunks"] == prof["chunks"]) == pinned
     ctx.close()
