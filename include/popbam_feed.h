@@ -107,12 +107,41 @@ int  pbf_pileup_mt(const char *bam_path, int n_threads, int32_t chunk, int tid, 
 int  pbf_pack(const pbf_batch *raw, int n_samples, const pbf_filter *f, pbf_keys *out);
 void pbf_keys_free(pbf_keys *keys);
 
-/* pbf_pileup_mt + pbf_pack: each thread packs its own pieces, so the raw reads of the whole
- * region are never held at once.  Same batch as pbf_pack(pbf_pileup_mt(...)).            */
+/* pbf_pileup_mt + pbf_pack, through the piece stream below (pbf_kstream_*) merged into one
+ * batch: the raw reads of the whole region are never held at once.  Same batch as
+ * pbf_pack(pbf_pileup_mt(...)).                                                           */
 int  pbf_pileup_keys_mt(const char *bam_path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
                         int32_t win_size, const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg,
                         int32_t fallback_sample, int n_samples, int max_depth, const pbf_filter *f,
                         pbf_keys *out);
+
+/* The key batch of a region as a stream of pieces in position order (what pbf_pileup_keys_mt
+ * merges): `n_threads` workers, each with its own handle on `bam_path`, walk `chunk`-position
+ * pieces ahead of the consumer (at most 2 * n_threads pieces wait), so the consumer can hand
+ * each piece to the GPU (pbg_stream_push) while the next ones are walked.  A piece is walked
+ * once from its own records (the reads spanning each position in file order: bam_plp's buffer)
+ * unless a read can meet a full buffer (maxcnt), then window by window as pbf_pileup_mt does.
+ * Records are parsed into one arena per piece and each read group is resolved to its sample
+ * once per record.  pbf_kstream_next returns 1 with the next piece (release it with
+ * pbf_keys_free), 0 after the last, or the first failing piece's error.  `refseq` must stay
+ * valid until pbf_kstream_close.                                                           */
+typedef struct pbf_kstream pbf_kstream;
+typedef struct {
+    double   t_wall;             /* seconds since pbf_kstream_open                            */
+    double   t_fetch;            /* thread-seconds: index seek + BGZF inflate + record decode */
+    double   t_inflate;          /* ... of which inflate                                      */
+    double   t_walk;             /* thread-seconds: pileup walk + call_base's per-read loop   */
+    double   t_consumer_wait;    /* seconds pbf_kstream_next waited for a piece               */
+    uint64_t bytes_compressed, bytes_inflated, records;
+    uint32_t threads, pieces, crowded_pieces, _pad;
+} pbf_profile;
+int  pbf_kstream_open(const char *bam_path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end,
+                      int32_t win_size, const char *refseq, const char *const *rg_ids, const int32_t *rg_sample,
+                      int n_rg, int32_t fallback_sample, int n_samples, int max_depth, const pbf_filter *f,
+                      pbf_kstream **out);
+int  pbf_kstream_next(pbf_kstream *ks, pbf_keys *piece);
+int  pbf_kstream_profile(pbf_kstream *ks, pbf_profile *prof);
+void pbf_kstream_close(pbf_kstream *ks);
 
 /* fai_fetch: the whole sequence of contig `name` (case preserved, line breaks removed).
  * *seq is malloc'ed (NUL-terminated); free with pbf_free.                                 */

@@ -124,6 +124,15 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
                 }
                 d.sample_pop[v] = (int8_t)i;
             }
+    {   // samples grouped by population (window statistics: per-population-pair loops)
+        int at = 0;
+        for (int i = 0; i < p->n_pops; ++i) {
+            d.pop_start[i] = (int16_t)at;
+            for (int v = 0; v < p->n_samples; ++v)
+                if (d.sample_pop[v] == i) d.pop_member[at++] = (uint8_t)v;
+        }
+        for (int i = p->n_pops; i <= PBG_MAX_POPS; ++i) d.pop_start[i] = (int16_t)at;
+    }
     for (int k = 0; k <= PBG_FAST_MAX; ++k) d.rms_thr[k] = rms_threshold(k, p->min_rmsQ, p->min_depth, p->max_depth);
     d.rmsq_thr[0] = p->min_rmsQ <= 0 ? 0u : 0xFFFFFFFFu;
     for (int k = 1; k <= 16; ++k) d.rmsq_thr[k] = rms_threshold(k, p->min_rmsQ, 1, 1 << 30);
@@ -423,10 +432,12 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     const uint64_t mw = c->row_bytes == 16 ? 2 : 1;
     bool known = false;
     uint64_t zstride = 0;
+    int segcap = pbg::kSegCap;
     for (const auto &pl : c->plans)
         if (pl.wins == (const void *)wins && pl.n_win == n_win && pl.n_rows == n_rows && pl.stats == o->stats) {
             known = true;
             zstride = pl.zstride;
+            segcap = pl.segcap;
         }
     if (!known) {
         std::vector<pbg_window> hw(n_win);
@@ -437,10 +448,16 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
         for (uint32_t i = 0; i < n_win; ++i) {
             if (hw[i].beg < 0 || hw[i].end < hw[i].beg || (uint32_t)hw[i].end > n_rows)
                 return fail(c, PBG_E_RANGE, "window outside the row range");
+            maxlen = std::max<uint64_t>(maxlen, (uint64_t)(hw[i].end - hw[i].beg));
+        }
+        // segregating rows each window keeps in LDS: short windows need few, and a smaller slice
+        // leaves room for more waves per CU (1 kb windows at 96 samples: 64 rows, 1 KB of masks);
+        // windows with more spill to the pool
+        segcap = maxlen <= 2048 ? 64 : maxlen <= 8192 ? 128 : pbg::kSegCap;
+        for (uint32_t i = 0; i < n_win; ++i) {
             const uint64_t len = (uint64_t)(hw[i].end - hw[i].beg);
-            maxlen = std::max(maxlen, len);
             // words: masks are mw words each (two for 16-byte rows)
-            if (ld_ws || len > (uint64_t)pbg::kSegCap) worst += mw * len + (uint64_t)n * (len / 64 + 1) + (ld_ws ? mw * np * len : 0);
+            if (ld_ws || len > (uint64_t)segcap) worst += mw * len + (uint64_t)n * (len / 64 + 1) + (ld_ws ? mw * np * len : 0);
             if (o->stats & PBG_S_ZNS) worst += mw * np * len;
         }
         constexpr uint64_t kPoolMax = 512ull << 20;   // words (4 GiB)
@@ -482,7 +499,7 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
             }
         }
         if (c->plans.size() >= 16) c->plans.erase(c->plans.begin());
-        c->plans.push_back({wins, n_win, n_rows, o->stats, zstride});
+        c->plans.push_back({wins, n_win, n_rows, o->stats, zstride, segcap});
     }
     A.pool = c->d_ws;
     A.pool_cap = c->ws_cap / 8;
@@ -496,7 +513,7 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     A.seg_count = c->d_segcnt;
     A.var_count = c->d_segcnt + n_win;
     A.ld_ns = c->d_segcnt + n_win + (size_t)n_win * np;
-    A.lds = pbg::stats_lds_layout(n, np, c->dp.sfs_stride, o->stats, 0, (int)mw);
+    A.lds = pbg::stats_lds_layout(n, np, c->dp.sfs_stride, o->stats, 0, (int)mw, segcap);
     if (A.lds.bytes > 64 * 1024) return fail(c, PBG_E_ARG, "statistics need more LDS than a workgroup has");
     HIPCHK(c, pbg::launch_window_stats(c->row_bytes, c->dp, c->dt, rows, n_rows, n_win, A, (hipStream_t)stream, c->n_cu));
     return PBG_OK;

@@ -14,14 +14,20 @@
 //                 each resolved to a query position / deletion / ref-skip (resolve_cigar2,
 //                 :90-235);
 //   popbam.cpp    the per-sample partition of call_base (:220-249).
+#include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <zlib.h>
 
 #include <algorithm>
-#include <thread>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <string>
+#include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -37,6 +43,67 @@ int fail(int code, const std::string &m) {
     return code;
 }
 
+using Clock = std::chrono::steady_clock;
+double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+// ---------------------------------------------------------------- raw deflate
+// BGZF blocks are raw deflate streams of at most 64 KB.  libdeflate (a system library of this
+// image, loaded at run time: its header is not installed) inflates a whole block in one call
+// about twice as fast as zlib; zlib's inflate (one reused stream per reader) is the fallback.
+struct LibDeflate {
+    void *(*alloc)() = nullptr;
+    int (*run)(void *, const void *, size_t, void *, size_t, size_t *) = nullptr;
+    void (*free_)(void *) = nullptr;
+};
+const LibDeflate &libdeflate() {
+    static LibDeflate ld = [] {
+        LibDeflate x;
+        if (getenv("POPBAM_NO_LIBDEFLATE")) return x;
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return x;
+        x.alloc = (void *(*)())dlsym(h, "libdeflate_alloc_decompressor");
+        x.run = (int (*)(void *, const void *, size_t, void *, size_t, size_t *))dlsym(h, "libdeflate_deflate_decompress");
+        x.free_ = (void (*)(void *))dlsym(h, "libdeflate_free_decompressor");
+        if (!x.alloc || !x.run || !x.free_) x = LibDeflate{};
+        return x;
+    }();
+    return ld;
+}
+struct Inflater {
+    void *ld = nullptr;
+    z_stream zs;
+    bool zinit = false;
+    Inflater() {
+        if (libdeflate().alloc) ld = libdeflate().alloc();
+    }
+    ~Inflater() {
+        if (ld) libdeflate().free_(ld);
+        if (zinit) inflateEnd(&zs);
+    }
+    Inflater(const Inflater &) = delete;
+    Inflater &operator=(const Inflater &) = delete;
+    // true when `in` inflates to exactly `out_n` bytes
+    bool run(const uint8_t *in, size_t n, uint8_t *out, size_t out_n) {
+        if (ld) {
+            size_t got = 0;
+            return libdeflate().run(ld, in, n, out, out_n, &got) == 0 && got == out_n;
+        }
+        if (!zinit) {
+            memset(&zs, 0, sizeof(zs));
+            if (inflateInit2(&zs, -15) != Z_OK) return false;
+            zinit = true;
+        } else if (inflateReset(&zs) != Z_OK) {
+            return false;
+        }
+        zs.next_in = const_cast<uint8_t *>(in);
+        zs.avail_in = (uInt)n;
+        zs.next_out = out;
+        zs.avail_out = (uInt)out_n;
+        const int r = inflate(&zs, Z_FINISH);
+        return r == Z_STREAM_END && zs.avail_out == 0;
+    }
+};
+
 // ---------------------------------------------------------------- BGZF
 struct Bgzf {
     FILE *f = nullptr;
@@ -44,14 +111,19 @@ struct Bgzf {
     size_t at = 0;                // read position in blk
     uint64_t blk_addr = 0;        // file offset of the current block
     uint64_t next_addr = 0;       // file offset of the next block
+    uint64_t fpos = ~0ull;        // the FILE's position (a block after the previous one needs no seek)
     std::vector<uint8_t> cbuf;
+    Inflater inf;
+    double t_inflate = 0.0;       // seconds in inflate
+    uint64_t n_blocks = 0, bytes_in = 0, bytes_out = 0;
 
     ~Bgzf() {
         if (f) fclose(f);
     }
     // loads the block at file offset `addr`; false at EOF, throws nothing
     int load(uint64_t addr) {
-        if (fseeko(f, (off_t)addr, SEEK_SET) != 0) return fail(PBF_E_IO, "seek failed");
+        if (addr != fpos && fseeko(f, (off_t)addr, SEEK_SET) != 0) return fail(PBF_E_IO, "seek failed");
+        fpos = ~0ull;
         uint8_t h[18];
         size_t got = fread(h, 1, 18, f);
         blk.clear();
@@ -64,9 +136,9 @@ struct Bgzf {
         if (got < 18 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4))
             return fail(PBF_E_FORMAT, "not a BGZF block");
         const int xlen = h[10] | h[11] << 8;
-        std::vector<uint8_t> extra(xlen);
-        memcpy(extra.data(), h + 12, std::min(xlen, 6));
-        if (xlen > 6 && fread(extra.data() + 6, 1, xlen - 6, f) != (size_t)(xlen - 6))
+        uint8_t extra[65536 + 6];
+        memcpy(extra, h + 12, std::min(xlen, 6));
+        if (xlen > 6 && fread(extra + 6, 1, xlen - 6, f) != (size_t)(xlen - 6))
             return fail(PBF_E_FORMAT, "truncated BGZF header");
         int bsize = -1;
         for (int p = 0; p + 4 <= xlen;) {
@@ -85,17 +157,15 @@ struct Bgzf {
                                (uint32_t)cbuf[cdata + 7] << 24;
         blk.resize(isize);
         next_addr = addr + (uint64_t)bsize + 1;
+        fpos = next_addr;
         if (isize == 0) return 1;
-        z_stream zs;
-        memset(&zs, 0, sizeof(zs));
-        if (inflateInit2(&zs, -15) != Z_OK) return fail(PBF_E_FORMAT, "inflateInit2");
-        zs.next_in = cbuf.data();
-        zs.avail_in = (uInt)cdata;
-        zs.next_out = blk.data();
-        zs.avail_out = isize;
-        const int r = inflate(&zs, Z_FINISH);
-        inflateEnd(&zs);
-        if (r != Z_STREAM_END || zs.avail_out != 0) return fail(PBF_E_FORMAT, "corrupt BGZF block");
+        const auto t0 = Clock::now();
+        const bool ok = inf.run(cbuf.data(), (size_t)cdata, blk.data(), isize);
+        t_inflate += secs(t0, Clock::now());
+        ++n_blocks;
+        bytes_in += (uint64_t)cdata;
+        bytes_out += isize;
+        if (!ok) return fail(PBF_E_FORMAT, "corrupt BGZF block");
         return 1;
     }
     int seek(uint64_t voff) {
@@ -375,6 +445,7 @@ int pbf_open(pbf_bam **out, const char *path) {
         delete b;
         return fail(PBF_E_IO, std::string("cannot open ") + path);
     }
+    setvbuf(b->z.f, nullptr, _IOFBF, 1 << 20);
     int r = b->z.load(0);
     if (r <= 0) {
         delete b;
@@ -699,6 +770,621 @@ int piece_batch(pbf_bam *b, int tid, int32_t cb, int32_t ce, int32_t rbeg, int32
     return batch_finish(out, cf.ns, o.reads);
 }
 
+
+// ---------------------------------------------------------------- key batches, fast path
+// The key batch of a piece straight from the records: no per-record heap objects (records are
+// parsed into one arena per piece), the read group resolved to a sample once per record (the
+// reference's bam_aux_get + khash lookup per read per position, popbam.cpp:222-237), and the
+// pileup walked with the reads that span each position kept in push (file) order -- the
+// buffer bam_plp_push / bam_plp_next keep (bam_pileup.c:283-407) whenever no read meets a full
+// buffer (maxcnt), which pieces where one can fall back to the window-by-window walk above.
+
+struct Rec2 {
+    int32_t tid, pos, end;   // end = bam_calend
+    uint16_t flag, n_cigar;
+    uint8_t mapq, strand;
+    int32_t l_seq;
+    int32_t sample;          // >= 0; -1 no RG (skipped); -2 RG not assigned to a sample
+    size_t off;              // arena: cigar (n_cigar u32), packed seq ((l_seq + 1) / 2), qual (l_seq), RG (NUL-terminated)
+};
+struct Arena {   // grows without zero-filling (every byte is written before it is read)
+    uint8_t *p = nullptr;
+    size_t n = 0, cap = 0;
+    ~Arena() { free(p); }
+    uint8_t *grow(size_t k) {
+        if (n + k > cap) {
+            const size_t nc = std::max(n + k, cap * 2 + (1 << 20));
+            uint8_t *q = (uint8_t *)realloc(p, nc);
+            if (!q) return nullptr;
+            p = q;
+            cap = nc;
+        }
+        uint8_t *at = p + n;
+        n += k;
+        return at;
+    }
+    const uint8_t *data() const { return p; }
+    size_t size() const { return n; }
+};
+struct RecSet {
+    std::vector<Rec2> r;
+    Arena arena;
+    std::vector<uint8_t> scratch;
+    void clear() {
+        r.clear();
+        arena.n = 0;
+    }
+};
+
+// the sample of a read group (the callback's partition, popbam.cpp:222-237), looked up without
+// copying the tag (views into the WalkCfg's keys, which outlive the index)
+struct RgIndex {
+    std::unordered_map<std::string_view, int32_t> m;
+    int32_t fallback;
+    int ns;
+    explicit RgIndex(const WalkCfg &cf) : fallback(cf.fallback), ns(cf.ns) {
+        for (const auto &kv : cf.rgmap) m[std::string_view(kv.first)] = kv.second;
+    }
+    int32_t sample_of(const char *rg, bool has_rg) const {
+        if (!has_rg) return -1;
+        auto it = m.find(std::string_view(rg));
+        const int32_t s = it != m.end() ? it->second : fallback;
+        return (s < 0 || s >= ns) ? -2 : s;
+    }
+};
+
+// bam_read1 into the arena: 1 = record (kept when of `tid` and overlapping [lo, hi)), 0 = EOF,
+// 2 = past the region (stop), < 0 error
+int read_rec2(Bgzf &z, RecSet &rs, int tid, int32_t lo, int32_t hi, bool has_index, const RgIndex &cf) {
+    uint8_t b4[4];
+    const long g = z.read(b4, 4);
+    if (g == 0) return 0;
+    if (g != 4) return fail(PBF_E_FORMAT, "truncated BAM record");
+    const uint32_t bs = le32(b4);
+    if (bs < 32) return fail(PBF_E_FORMAT, "bad BAM record size");
+    if (rs.scratch.size() < bs) rs.scratch.resize(bs);
+    if (z.read(rs.scratch.data(), bs) != (long)bs) return fail(PBF_E_FORMAT, "truncated BAM record");
+    const uint8_t *p = rs.scratch.data(), *e = p + bs;
+    Rec2 r;
+    r.tid = (int32_t)le32(p);
+    r.pos = (int32_t)le32(p + 4);
+    if (r.tid != tid) return (has_index || r.tid > tid) ? 2 : 1;   // sorted: past the contig (or skip)
+    if (r.pos >= hi) return 2;
+    const uint32_t bin_mq_nl = le32(p + 8), flag_nc = le32(p + 12);
+    const int32_t l_seq = (int32_t)le32(p + 16);
+    const int l_name = bin_mq_nl & 0xFF;
+    r.mapq = (uint8_t)((bin_mq_nl >> 8) & 0xFF);
+    r.flag = (uint16_t)(flag_nc >> 16);
+    r.strand = (uint8_t)((r.flag >> 4) & 1u);
+    const int n_cig = flag_nc & 0xFFFF;
+    const uint8_t *q = p + 32 + l_name;
+    if (l_seq < 0 || q + 4 * (size_t)n_cig + (l_seq + 1) / 2 + l_seq > e)
+        return fail(PBF_E_FORMAT, "BAM record fields exceed its size");
+    int32_t end = r.pos;
+    for (int i = 0; i < n_cig; ++i) {
+        const uint32_t c = le32(q + 4 * i), op = c & 0xF;
+        if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) end += (int32_t)(c >> 4);
+    }
+    r.end = end;
+    const int32_t oend = n_cig ? end : r.pos + 1;
+    if (!(oend > lo && r.pos < hi)) return 1;   // not overlapping (is_overlap, bam_index.c:729-735)
+    r.n_cigar = (uint16_t)n_cig;
+    r.l_seq = l_seq;
+    const uint8_t *aux = q + 4 * (size_t)n_cig + (l_seq + 1) / 2 + l_seq;
+    const char *rg = nullptr;
+    bool has_rg = false;
+    for (const uint8_t *a = aux; a + 3 <= e;) {   // bam_aux_get(b, "RG")
+        const char t = (char)a[2];
+        const size_t sz = aux_size(t, a + 3, e);
+        if (!sz) break;
+        if (a[0] == 'R' && a[1] == 'G') {
+            has_rg = true;
+            rg = (t == 'Z' || t == 'H') ? (const char *)a + 3 : "";   // non-string RG: its raw bytes (feeder.cpp Rec)
+            break;
+        }
+        a += 3 + sz;
+    }
+    r.sample = cf.sample_of(rg ? rg : "", has_rg);
+    const size_t rglen = r.sample == -2 ? strlen(rg) + 1 : 0;   // kept for the error message only
+    const size_t need = 4 * (size_t)n_cig + (l_seq + 1) / 2 + l_seq + rglen;
+    r.off = rs.arena.size();
+    uint8_t *dst = rs.arena.grow(need);
+    if (!dst) return fail(PBF_E_IO, "out of host memory");
+    memcpy(dst, q, need - rglen);
+    if (rglen) memcpy(dst + need - rglen, rg, rglen);
+    rs.r.push_back(r);
+    return 1;
+}
+
+// bam_fetch into the arena: reads of `tid` overlapping [lo, hi) in file order
+int fetch2(pbf_bam *b, int tid, int32_t lo, int32_t hi, const RgIndex &cf, RecSet &rs) {
+    rs.clear();
+    uint64_t start;
+    if (hi <= lo || !region_start(b, tid, lo, hi, start)) return PBF_OK;
+    int r = b->z.seek(start);
+    if (r < 0) return r;
+    while ((r = read_rec2(b->z, rs, tid, lo, hi, b->has_index, cf)) == 1) {
+    }
+    return r < 0 ? r : PBF_OK;
+}
+
+// resolve_cigar2 (bam_pileup.c:90-235) on a Rec2, the cursor kept in (k, x, y) as Node does
+struct Cur {
+    const Rec2 *r;
+    int k;
+    int32_t x, y;
+};
+inline int resolve2(Cur &n, const uint32_t *cg, int32_t pos, int32_t *qpos) {
+    const int nc = n.r->n_cigar;
+    if (n.k < 0) {
+        n.x = n.r->pos;
+        n.y = 0;
+        int k = 0;
+        for (; k < nc; ++k) {
+            const uint32_t op = cg[k] & 0xF, l = cg[k] >> 4;
+            if (op == 0 || op == 2 || op == 7 || op == 8) break;
+            if (op == 3) n.x += (int32_t)l;
+            else if (op == 1 || op == 4) n.y += (int32_t)l;
+        }
+        n.k = k < nc ? k : nc - 1;
+    }
+    for (;;) {
+        const uint32_t op = cg[n.k] & 0xF, l = cg[n.k] >> 4;
+        const bool cons_ref = op == 0 || op == 2 || op == 3 || op == 7 || op == 8;
+        if (cons_ref && pos - n.x < (int32_t)l) break;
+        if (n.k + 1 >= nc) break;
+        if (op == 0 || op == 7 || op == 8 || op == 1 || op == 4) n.y += (int32_t)l;
+        if (cons_ref) n.x += (int32_t)l;
+        ++n.k;
+    }
+    const uint32_t op = cg[n.k] & 0xF;
+    if (op == 2) return 1;
+    if (op == 3) return 2;
+    *qpos = n.y + (pos - n.x);
+    return 0;
+}
+
+// growable 16-byte aligned key buffer (malloc'ed: pbf_keys_free releases it)
+struct KeyBuf {
+    uint16_t *p = nullptr;
+    size_t n = 0, cap = 0;
+    ~KeyBuf() { free(p); }
+    bool reserve(size_t want) {
+        if (want <= cap) return true;
+        size_t nc = std::max<size_t>(want, cap + cap / 2 + 1024);
+        nc = (nc + 7) & ~(size_t)7;
+        uint16_t *q = (uint16_t *)aligned_alloc(16, nc * 2);
+        if (!q) return false;
+        if (n) memcpy(q, p, n * 2);
+        free(p);
+        p = q;
+        cap = nc;
+        return true;
+    }
+    uint16_t *release() {
+        uint16_t *q = p;
+        p = nullptr;
+        n = cap = 0;
+        return q;
+    }
+};
+
+// Positions [cb, ce) of one walk of `rs` (every read kept: no maxcnt drop can occur) into a key
+// batch: per position the reads that span it in file order (the pileup buffer), each resolved
+// to a query position; deletions / ref skips / reads without RG are skipped, an RG without a
+// sample is the reference's fatal error, the first max_depth reads of a sample are its reads,
+// and call_base's per-read loop keeps those passing the baseQ / mapQ / N filters as keys.
+// A read's per-position outcome is resolved once, when it joins the buffer: one u16 code per
+// position it spans in [cb, ce) (0xFFFF: no base there -- deletion / ref skip; else its key, 0
+// when call_base's filters drop it but it still counts against max_depth), so a position costs
+// one code load per buffered read.
+constexpr uint16_t kNoBase = 0xFFFF;
+struct Act {
+    const uint16_t *code;   // code[pos] for pos in [joined, end)
+    int32_t end;
+    int32_t sample;
+    uint32_t mq2;
+    uint32_t rec;           // index in rs.r
+};
+// call_base's key of a base as a function of (quality byte, nt16) for one (mapQ, strand): a
+// 4096-entry table per pair, built when first needed
+struct KeyLut {
+    std::vector<std::vector<uint16_t>> t = std::vector<std::vector<uint16_t>>(512);
+    const uint16_t *get(uint32_t mapq, uint32_t strand, uint32_t minb, uint32_t minm, bool ill) {
+        std::vector<uint16_t> &v = t[(mapq << 1) | strand];
+        if (v.empty()) {
+            v.resize(4096);
+            for (uint32_t q = 0; q < 256; ++q)
+                for (uint32_t nt = 0; nt < 16; ++nt)
+                    v[q << 4 | nt] = (uint16_t)pbg::read_to_key(q | mapq << 8 | nt << 16 | strand << 20, minb, minm, ill);
+        }
+        return v.data();
+    }
+};
+int fast_walk(const RecSet &rs, int32_t cb, int32_t ce, const WalkCfg &cf, const pbf_filter &f, std::vector<uint16_t> &codes,
+              KeyLut &lut, pbf_keys *out) {
+    const int ns = cf.ns, kb = f.k_bytes;
+    const uint32_t L = (uint32_t)(ce - cb);
+    const uint32_t minb = (uint32_t)(f.min_baseQ & 0xff), minm = (uint32_t)(f.min_mapQ & 0xff);
+    const bool ill = f.illumina != 0;
+    const uint32_t md = (uint32_t)std::max(0, cf.max_depth);
+    KeyBuf keys;
+    // the codes of every read over [cb, ce): their total is the keys' upper bound
+    size_t ncode = 0;
+    for (const Rec2 &r : rs.r)
+        if (!(r.tid < 0 || (r.flag & kDefMask)) && r.end > cb && r.pos < ce)
+            ncode += (size_t)(std::min(r.end, ce) - std::max(r.pos, cb));
+    if (codes.size() < ncode + 1) codes.resize(ncode + 1);
+    if (!keys.reserve(ncode + 8)) return fail(PBF_E_IO, "out of host memory");
+    size_t cfill = 0;
+    const uint8_t *ar = rs.arena.data();
+    // resolve_cigar2 + call_base's key for each position of [a, b) a read spans
+    auto fill = [&](const Rec2 &r, int32_t a, int32_t b, uint16_t *dst) {
+        const uint8_t *rec = ar + r.off;
+        const uint32_t *cg = reinterpret_cast<const uint32_t *>(rec);
+        const uint8_t *seq = rec + 4 * (size_t)r.n_cigar, *qual = seq + (r.l_seq + 1) / 2;
+        const uint16_t *kl = lut.get(r.mapq, r.strand, minb, minm, ill);
+        auto key_at = [&](int32_t qp) -> uint16_t {
+            if (qp < 0 || qp >= r.l_seq) return 0;   // a CIGAR past its sequence (the reference reads past it)
+            return kl[(uint32_t)qual[qp] << 4 | ((seq[qp >> 1] >> ((~qp & 1) << 2)) & 0xFu)];
+        };
+        const uint32_t op0 = cg[0] & 0xF;
+        if (r.n_cigar == 1 && (op0 == 0 || op0 == 7 || op0 == 8)) {   // one M / = / X: query pos = p - pos
+            const int32_t q1 = std::min(b - r.pos, r.l_seq);
+            uint16_t *d = dst;
+            int32_t qp = a - r.pos;
+            if (qp < q1 && (qp & 1)) *d++ = key_at(qp++);
+            for (; qp + 1 < q1; qp += 2) {   // two bases per sequence byte
+                const uint32_t sb = seq[qp >> 1];
+                d[0] = kl[(uint32_t)qual[qp] << 4 | (sb >> 4)];
+                d[1] = kl[(uint32_t)qual[qp + 1] << 4 | (sb & 0xFu)];
+                d += 2;
+            }
+            if (qp < q1) *d++ = key_at(qp++);
+            for (int32_t p = r.pos + std::max(qp, q1); p < b; ++p) *d++ = 0;   // past the sequence
+            return;
+        }
+        Cur cur{&r, -1, 0, 0};
+        for (int32_t p = a; p < b; ++p) {
+            int32_t qp = 0;
+            const int kind = r.n_cigar ? resolve2(cur, cg, p, &qp) : 1;
+            dst[p - a] = kind != 0 ? kNoBase : key_at(qp);
+        }
+    };
+    // the buffer, split by sample (each list in file order = the buffer's order); reads without
+    // RG never reach a sample but still make their positions called back (`cover`, a difference
+    // array over [cb, ce]); a read whose RG has no sample is the fatal error at its first base
+    std::vector<std::vector<Act>> lists(ns);
+    for (auto &l : lists) l.reserve(64);
+    std::vector<int32_t> cover((size_t)L + 1, 0);
+    int64_t bad_pos = INT64_MAX;
+    size_t bad_rec = 0;
+    size_t idx = 0;
+    const size_t nrec = rs.r.size();
+    uint8_t *kout = (uint8_t *)out->k;
+    uint32_t *rout = out->rmsq;
+    int32_t live = 0;   // coverage at pos
+    for (int32_t pos = cb; pos < ce;) {
+        const uint32_t i = (uint32_t)(pos - cb);
+        if ((i & 63u) == 0) out->block_off[i >> 6] = keys.n;
+        // reads starting at or before pos join the buffer in file order
+        while (idx < nrec && rs.r[idx].pos <= pos) {
+            const Rec2 &r = rs.r[idx++];
+            if (r.tid < 0 || (r.flag & kDefMask) || r.end <= pos) continue;
+            const int32_t b = std::min(r.end, ce);
+            ++cover[i];
+            --cover[(uint32_t)(b - cb)];
+            if (r.sample == -1) continue;   // no RG: skipped by the partition
+            uint16_t *dst = codes.data() + cfill;
+            fill(r, pos, b, dst);
+            cfill += (size_t)(b - pos);
+            if (r.sample < 0) {   // its first base in [pos, b), if any, is where the reference stops
+                for (int32_t p = pos; p < b; ++p)
+                    if (dst[p - pos] != kNoBase) {
+                        if (p < bad_pos) bad_pos = p, bad_rec = idx - 1;
+                        break;
+                    }
+                continue;
+            }
+            lists[r.sample].push_back(Act{dst - pos, b, r.sample, (uint32_t)r.mapq * r.mapq, (uint32_t)(idx - 1)});
+        }
+        live += cover[i];
+        if (live == 0) {   // no read spans pos: no callback until the next read starts
+            const int32_t nxt = idx < nrec ? std::max(pos + 1, std::min(ce, rs.r[idx].pos)) : ce;
+            for (int32_t q = pos + 1; q < nxt; ++q) {
+                const uint32_t iq = (uint32_t)(q - cb);
+                live += cover[iq];   // (zero: nothing starts or ends in between)
+                if ((iq & 63u) == 0) out->block_off[iq >> 6] = keys.n;
+            }
+            pos = nxt;
+            continue;
+        }
+        out->ref[i] &= 0x7F;   // a read spans pos: the pileup calls back here
+        const size_t t0 = (size_t)i * ns;
+        uint16_t *kd = keys.p + keys.n;
+        size_t nk = 0;
+        for (int s = 0; s < ns; ++s) {
+            std::vector<Act> &l = lists[s];
+            const size_t na = l.size();
+            Act *A = l.data();
+            size_t w = 0;
+            uint32_t raw = 0, kk = 0, rq = 0;
+            for (size_t j = 0; j < na; ++j) {
+                const Act a = A[j];
+                if (a.end <= pos) continue;   // finished: leaves the buffer
+                A[w++] = a;
+                const uint16_t c = a.code[pos];
+                if (c == kNoBase || raw >= md) continue;   // no base here; past the sample's max_depth reads
+                ++raw;
+                kd[nk] = c;
+                nk += c != 0;
+                kk += c != 0;
+                rq += c ? a.mq2 : 0u;   // rmsq += SQ(core.qual) (popbam.cpp:287)
+            }
+            l.resize(w);
+            if (kb == 1) {
+                if (kk > 255) return fail(PBF_E_ARG, "more than 255 keys per sample need k_bytes = 2");
+                kout[t0 + s] = (uint8_t)kk;
+            } else {
+                reinterpret_cast<uint16_t *>(kout)[t0 + s] = (uint16_t)kk;
+            }
+            rout[t0 + s] = rq;
+        }
+        keys.n += nk;
+        ++pos;
+    }
+    out->block_off[(L + 63) / 64] = keys.n;
+    out->n_keys = keys.n;
+    out->keys = keys.release();
+    if (bad_pos != INT64_MAX) {
+        const Rec2 &r = rs.r[bad_rec];
+        const char *rg = (const char *)ar + r.off + 4 * (size_t)r.n_cigar + (r.l_seq + 1) / 2 + r.l_seq;
+        return fail(PBF_E_RG, std::string("Problem assigning read group ") + rg +
+                                  " to a sample.\nPlease check BAM header for correct SM and PO tags");
+    }
+    return PBF_OK;
+}
+
+struct PieceProf {
+    double t_fetch = 0, t_inflate = 0, t_walk = 0;
+    uint64_t bytes_in = 0, bytes_out = 0, records = 0;
+    uint32_t crowded = 0;
+};
+
+// one piece [cb, ce) of a region as a key batch: the fast walk, or (a read can meet a full
+// buffer) the reference's window-by-window walks + pbf_pack
+int piece_keys(pbf_bam *b, int tid, int32_t cb, int32_t ce, int32_t rbeg, int32_t rend, int32_t win,
+               const char *refseq, const WalkCfg &cf, const pbf_filter &f, RecSet &rs, std::vector<uint16_t> &codes,
+               KeyLut &lut, pbf_keys *out, PieceProf &pp) {
+    memset(out, 0, sizeof(*out));
+    const uint32_t L = (uint32_t)(ce - cb);
+    const double inf0 = b->z.t_inflate;
+    const uint64_t bi0 = b->z.bytes_in, bo0 = b->z.bytes_out;
+    const auto t0 = Clock::now();
+    const RgIndex rgi(cf);
+    int r = fetch2(b, tid, std::max(0, cb - 1), ce, rgi, rs);
+    if (r != PBF_OK) return r;
+    int32_t lo = cb;
+    for (const Rec2 &x : rs.r)
+        if (!(x.flag & kDefMask)) lo = std::min(lo, x.pos);
+    // the buffer bound of chunk_walk (max_buffer_bound) on the reads that reach cb
+    int bound = 0;
+    {
+        std::vector<int32_t> ends;
+        auto scan = [&](const Rec2 &x) {
+            if (x.tid < 0 || (x.flag & kDefMask)) return;
+            while (!ends.empty() && ends.front() < x.pos) {
+                std::pop_heap(ends.begin(), ends.end(), std::greater<int32_t>());
+                ends.pop_back();
+            }
+            if (x.pos >= cb || x.end >= cb) bound = std::max(bound, (int)ends.size());
+            ends.push_back(std::max(x.end, x.pos + 1));
+            std::push_heap(ends.begin(), ends.end(), std::greater<int32_t>());
+        };
+        if (lo < cb) {   // the reads before cb that reach it: their tests see reads ending before cb too
+            RecSet early;
+            r = fetch2(b, tid, std::max(0, lo - 1), cb, rgi, early);
+            if (r != PBF_OK) return r;
+            for (const Rec2 &x : early.r)
+                if (x.pos < cb) scan(x);
+        }
+        for (const Rec2 &x : rs.r)
+            if (lo >= cb || x.pos >= cb) scan(x);
+    }
+    const auto t1 = Clock::now();
+    pp.t_fetch += secs(t0, t1);
+    pp.records += rs.r.size();
+    if (bound + 2 > kMaxCnt) {   // crowded: the reference's own walks, then call_base's per-read loop
+        ++pp.crowded;
+        pbf_batch raw;
+        r = piece_batch(b, tid, cb, ce, rbeg, rend, win, refseq, cf, &raw);
+        if (r == PBF_OK) {
+            r = pbf_pack(&raw, cf.ns, &f, out);
+            pbf_batch_free(&raw);
+        }
+    } else {
+        const size_t nt = (size_t)L * cf.ns;
+        out->n_sites = L;
+        out->pos0 = cb;
+        out->ref = (uint8_t *)malloc(std::max<size_t>(L, 1));
+        out->k = calloc(std::max<size_t>(nt, 1), f.k_bytes);
+        out->rmsq = (uint32_t *)calloc(std::max<size_t>(nt, 1), sizeof(uint32_t));
+        out->block_off = (uint64_t *)calloc(L / 64 + 2, sizeof(uint64_t));
+        if (!out->ref || !out->k || !out->rmsq || !out->block_off) {
+            pbf_keys_free(out);
+            return fail(PBF_E_IO, "out of host memory");
+        }
+        for (uint32_t i = 0; i < L; ++i) out->ref[i] = (uint8_t)refseq[cb + i] | 0x80;
+        r = fast_walk(rs, cb, ce, cf, f, codes, lut, out);
+        if (r != PBF_OK) pbf_keys_free(out);
+    }
+    pp.t_walk += secs(t1, Clock::now());
+    pp.t_inflate += b->z.t_inflate - inf0;
+    pp.bytes_in += b->z.bytes_in - bi0;
+    pp.bytes_out += b->z.bytes_out - bo0;
+    return r;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- piece stream
+// Pieces of a region walked by worker threads (each with its own file handle) and handed out in
+// position order; at most `lookahead` pieces wait, so host memory is bounded by the lookahead.
+struct pbf_kstream {
+    std::string path;
+    int tid = 0;
+    int32_t beg = 0, end = 0, win = 0, chunk = 0;
+    int64_t nchunk = 0;
+    const char *refseq = nullptr;
+    WalkCfg cf;
+    pbf_filter f{};
+    std::vector<pbf_keys> parts;
+    std::vector<int> state;        // 0 pending, 1 ready, 2 taken
+    std::vector<int> rc;
+    std::vector<std::string> msg;
+    std::mutex m;
+    std::condition_variable cv_ready, cv_space;
+    int64_t next = 0, consumed = 0, lookahead = 0;
+    bool stop = false;
+    std::vector<std::thread> th;
+    pbf_profile prof{};
+    Clock::time_point t_open;
+};
+
+namespace {
+
+void kstream_worker(pbf_kstream *ks) {
+    pbf_bam *b = nullptr;
+    int open_rc = pbf_open(&b, ks->path.c_str());
+    if (open_rc == PBF_OK && ks->tid >= (int)b->names.size()) open_rc = fail(PBF_E_ARG, "bad argument");
+    const std::string open_msg = open_rc ? g_err : std::string();
+    RecSet rs;
+    std::vector<uint16_t> codes;
+    KeyLut lut;
+    PieceProf pp;
+    for (;;) {
+        int64_t c;
+        {
+            std::unique_lock<std::mutex> lk(ks->m);
+            ks->cv_space.wait(lk, [&] { return ks->stop || ks->next >= ks->nchunk || ks->next < ks->consumed + ks->lookahead; });
+            if (ks->stop || ks->next >= ks->nchunk) break;
+            c = ks->next++;
+        }
+        const int32_t cb = (int32_t)(ks->beg + c * (int64_t)ks->chunk);
+        const int32_t ce = (int32_t)std::min<int64_t>(ks->end, ks->beg + (c + 1) * (int64_t)ks->chunk);
+        pbf_keys out;
+        memset(&out, 0, sizeof(out));
+        int r = open_rc;
+        std::string msg = open_msg;
+        pp = PieceProf{};
+        if (r == PBF_OK) {
+            r = piece_keys(b, ks->tid, cb, ce, ks->beg, ks->end, ks->win, ks->refseq, ks->cf, ks->f, rs, codes, lut, &out, pp);
+            if (r != PBF_OK) msg = g_err;
+        }
+        {
+            std::lock_guard<std::mutex> lk(ks->m);
+            ks->parts[c] = out;
+            ks->rc[c] = r;
+            ks->msg[c] = msg;
+            ks->state[c] = 1;
+            ks->prof.t_fetch += pp.t_fetch;
+            ks->prof.t_inflate += pp.t_inflate;
+            ks->prof.t_walk += pp.t_walk;
+            ks->prof.bytes_compressed += pp.bytes_in;
+            ks->prof.bytes_inflated += pp.bytes_out;
+            ks->prof.records += pp.records;
+            ks->prof.crowded_pieces += pp.crowded;
+        }
+        ks->cv_ready.notify_all();
+    }
+    if (b) pbf_close(b);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pbf_kstream_open(const char *path, int n_threads, int32_t chunk, int tid, int32_t beg, int32_t end, int32_t win_size,
+                     const char *refseq, const char *const *rg_ids, const int32_t *rg_sample, int n_rg, int32_t fallback,
+                     int ns, int max_depth, const pbf_filter *f, pbf_kstream **out) {
+    if (!out) return fail(PBF_E_ARG, "bad argument");
+    *out = nullptr;
+    if (!path || !refseq || !f || ns < 1 || end < beg || n_threads < 1 || tid < 0 || (f->k_bytes != 1 && f->k_bytes != 2))
+        return fail(PBF_E_ARG, "bad argument");
+    pbf_kstream *ks = new pbf_kstream();
+    ks->t_open = Clock::now();
+    ks->path = path;
+    ks->tid = tid;
+    ks->beg = beg;
+    ks->end = end;
+    ks->win = win_size;
+    if (chunk <= 0) chunk = 1 << 20;
+    ks->chunk = (chunk + 63) / 64 * 64;   // piece borders on 64-position blocks: block_off concatenates
+    ks->nchunk = std::max<int64_t>(1, ((int64_t)end - beg + ks->chunk - 1) / ks->chunk);
+    if (end == beg) ks->nchunk = 1;
+    ks->refseq = refseq;
+    ks->cf = make_cfg(rg_ids, rg_sample, n_rg, fallback, ns, max_depth);
+    ks->f = *f;
+    ks->parts.assign((size_t)ks->nchunk, pbf_keys{});
+    ks->state.assign((size_t)ks->nchunk, 0);
+    ks->rc.assign((size_t)ks->nchunk, PBF_OK);
+    ks->msg.assign((size_t)ks->nchunk, std::string());
+    const int nt = (int)std::min<int64_t>(n_threads, ks->nchunk);
+    ks->lookahead = std::max<int64_t>(2, 2 * (int64_t)nt);
+    ks->prof.threads = nt;
+    ks->prof.pieces = (uint32_t)ks->nchunk;
+    for (int w = 0; w < nt; ++w) ks->th.emplace_back(kstream_worker, ks);
+    *out = ks;
+    return PBF_OK;
+}
+
+int pbf_kstream_next(pbf_kstream *ks, pbf_keys *piece) {
+    if (!ks || !piece) return fail(PBF_E_ARG, "bad argument");
+    memset(piece, 0, sizeof(*piece));
+    std::unique_lock<std::mutex> lk(ks->m);
+    if (ks->consumed >= ks->nchunk) return 0;
+    const auto tw = Clock::now();
+    ks->cv_ready.wait(lk, [&] { return ks->state[ks->consumed] == 1; });
+    ks->prof.t_consumer_wait += secs(tw, Clock::now());
+    const int64_t c = ks->consumed;
+    ks->state[c] = 2;
+    if (ks->rc[c] != PBF_OK) {   // the first failing piece in position order (the sequential walk's error)
+        const int r = ks->rc[c];
+        const std::string msg = ks->msg[c];
+        lk.unlock();
+        return fail(r, msg);
+    }
+    *piece = ks->parts[c];
+    memset(&ks->parts[c], 0, sizeof(pbf_keys));
+    ++ks->consumed;
+    lk.unlock();
+    ks->cv_space.notify_all();
+    return 1;
+}
+
+int pbf_kstream_profile(pbf_kstream *ks, pbf_profile *p) {
+    if (!ks || !p) return fail(PBF_E_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(ks->m);
+    *p = ks->prof;
+    p->t_wall = secs(ks->t_open, Clock::now());
+    return PBF_OK;
+}
+
+void pbf_kstream_close(pbf_kstream *ks) {
+    if (!ks) return;
+    {
+        std::lock_guard<std::mutex> lk(ks->m);
+        ks->stop = true;
+    }
+    ks->cv_space.notify_all();
+    for (auto &t : ks->th) t.join();
+    for (auto &p : ks->parts) pbf_keys_free(&p);
+    delete ks;
+}
+
+}  // extern "C"
+
+namespace {
 }  // namespace
 
 extern "C" {
@@ -862,46 +1548,22 @@ int pbf_pileup_keys_mt(const char *path, int n_threads, int32_t chunk, int tid, 
     if (!path || !out || !refseq || !f || ns < 1 || end < beg || n_threads < 1 || tid < 0)
         return fail(PBF_E_ARG, "bad argument");
     memset(out, 0, sizeof(*out));
-    const WalkCfg cf = make_cfg(rg_ids, rg_sample, n_rg, fallback, ns, max_depth);
+    pbf_kstream *ks = nullptr;
+    int r = pbf_kstream_open(path, n_threads, chunk, tid, beg, end, win_size, refseq, rg_ids, rg_sample, n_rg, fallback, ns,
+                             max_depth, f, &ks);
+    if (r != PBF_OK) return r;
+    std::vector<pbf_keys> parts;
+    pbf_keys p;
+    while ((r = pbf_kstream_next(ks, &p)) == 1) parts.push_back(p);
+    const std::string msg = r < 0 ? g_err : std::string();
+    pbf_kstream_close(ks);
+    if (r < 0) {   // the first failing piece in position order
+        for (auto &q : parts) pbf_keys_free(&q);
+        return fail(r, msg);
+    }
     const int64_t L = (int64_t)end - beg;
-    if (chunk <= 0) chunk = 1 << 20;
-    chunk = (chunk + 63) / 64 * 64;   // chunk borders on 64-position blocks: block_off concatenates
-    const int64_t nchunk = std::max<int64_t>(1, (L + chunk - 1) / chunk);
-    std::vector<pbf_keys> parts((size_t)nchunk);
-    std::vector<int> rc((size_t)nchunk, PBF_OK);
-    std::vector<std::string> msg((size_t)nchunk);
-    for (auto &p : parts) memset(&p, 0, sizeof(p));
-    const int nt = (int)std::min<int64_t>(n_threads, nchunk);
-    auto worker = [&](int w) {
-        pbf_bam *b = nullptr;
-        int r = pbf_open(&b, path);
-        if (r == PBF_OK && tid >= (int)b->names.size()) r = fail(PBF_E_ARG, "bad argument");
-        for (int64_t c = w; c < nchunk; c += nt) {
-            if (r == PBF_OK) {
-                const int32_t cb = (int32_t)(beg + c * chunk), ce = (int32_t)std::min<int64_t>(end, beg + (c + 1) * chunk);
-                pbf_batch raw;
-                r = piece_batch(b, tid, cb, ce, beg, end, win_size, refseq, cf, &raw);
-                if (r == PBF_OK) {
-                    r = pbf_pack(&raw, ns, f, &parts[c]);
-                    pbf_batch_free(&raw);
-                }
-            }
-            rc[c] = r;
-            if (r != PBF_OK) msg[c] = g_err;
-        }
-        if (b) pbf_close(b);
-    };
-    std::vector<std::thread> th;
-    for (int w = 1; w < nt; ++w) th.emplace_back(worker, w);
-    worker(0);
-    for (auto &t : th) t.join();
-    for (int64_t c = 0; c < nchunk; ++c)
-        if (rc[c] != PBF_OK) {
-            for (auto &p : parts) pbf_keys_free(&p);
-            return fail(rc[c], msg[c]);
-        }
     uint64_t n_keys = 0;
-    for (auto &p : parts) n_keys += p.n_keys;
+    for (auto &q : parts) n_keys += q.n_keys;
     const int kb = f->k_bytes;
     out->n_sites = (uint32_t)L;
     out->pos0 = beg;
@@ -912,23 +1574,23 @@ int pbf_pileup_keys_mt(const char *path, int n_threads, int32_t chunk, int tid, 
     out->block_off = (uint64_t *)calloc((size_t)L / 64 + 2, sizeof(uint64_t));
     out->keys = (uint16_t *)aligned_alloc(16, (std::max<uint64_t>(n_keys, 1) * 2 + 15) & ~(size_t)15);
     if (!out->ref || !out->k || !out->rmsq || !out->block_off || !out->keys) {
-        for (auto &p : parts) pbf_keys_free(&p);
+        for (auto &q : parts) pbf_keys_free(&q);
         pbf_keys_free(out);
         return fail(PBF_E_IO, "out of host memory");
     }
     size_t site = 0;
     uint64_t koff = 0;
-    for (auto &p : parts) {   // each part is released as soon as it is copied
-        if (p.n_sites) {
-            memcpy(out->ref + site, p.ref, p.n_sites);
-            memcpy((char *)out->k + site * ns * kb, p.k, (size_t)p.n_sites * ns * kb);
-            memcpy(out->rmsq + site * ns, p.rmsq, (size_t)p.n_sites * ns * sizeof(uint32_t));
-            for (uint32_t bk = 0; bk * 64 < p.n_sites; ++bk) out->block_off[site / 64 + bk] = koff + p.block_off[bk];
+    for (auto &q : parts) {   // each part is released as soon as it is copied
+        if (q.n_sites) {
+            memcpy(out->ref + site, q.ref, q.n_sites);
+            memcpy((char *)out->k + site * ns * kb, q.k, (size_t)q.n_sites * ns * kb);
+            memcpy(out->rmsq + site * ns, q.rmsq, (size_t)q.n_sites * ns * sizeof(uint32_t));
+            for (uint32_t bk = 0; bk * 64 < q.n_sites; ++bk) out->block_off[site / 64 + bk] = koff + q.block_off[bk];
         }
-        if (p.n_keys) memcpy(out->keys + koff, p.keys, p.n_keys * sizeof(uint16_t));
-        site += p.n_sites;
-        koff += p.n_keys;
-        pbf_keys_free(&p);
+        if (q.n_keys) memcpy(out->keys + koff, q.keys, q.n_keys * sizeof(uint16_t));
+        site += q.n_sites;
+        koff += q.n_keys;
+        pbf_keys_free(&q);
     }
     out->block_off[((size_t)L + 63) / 64] = koff;
     return PBF_OK;

@@ -28,6 +28,8 @@ struct DevParams {
     int32_t k16;          // k[] is u16 (max_depth > 255), else u8
     int32_t sfs_stride;   // largest population + 1 (pbg_window_out.sfs_bins row)
     int8_t sample_pop[PBG_MAX_SAMPLES];   // population of each sample (-1: none); masks are disjoint
+    uint8_t pop_member[PBG_MAX_SAMPLES];  // the samples of population 0, then 1, ... (ascending within one)
+    int16_t pop_start[PBG_MAX_POPS + 1];  // population i's samples: pop_member[pop_start[i], pop_start[i+1])
     // qfilter of a reference-only sample with k = d keys (call_scan_kernel): it passes iff
     // sum mapQ^2 >= rms_thr[d].  rms = (unsigned)(sqrtf((float)rmsq / d) + 0.499) is monotone in
     // rmsq, so "rms >= min_rmsQ && min_depth <= d <= max_depth" is one threshold per d, found on
@@ -179,17 +181,19 @@ __host__ __device__ inline bool synth_all_pass(uint32_t min_baseQ, uint32_t min_
 }
 __host__ __device__ inline uint8_t synth_ref_char(const SynthSite &s) { return (uint8_t)"ACGT"[s.ref_idx]; }
 
-constexpr int kSegCap = 256;         // segregating rows kept in LDS per window (beyond: workspace)
+constexpr int kSegCap = 256;         // segregating rows kept in LDS per window (beyond: workspace), at most
 constexpr int kVarCap = 256;         // ZnS variable-site list kept in LDS per population
 
 // Dynamic LDS of window_stats_kernel (one wave per window): byte offsets of its arrays, sized
 // by the host for the sample / population counts and the statistics asked for.
 struct WinLds {
     uint32_t seg, var, plane, diff, acc, amin, bins, rbuf, r2, bytes;
-    int32_t planecap;   // bitplane words in LDS (n * kSegCap / 64)
+    int32_t segcap;     // segregating rows kept in LDS (a multiple of 64, <= kSegCap; beyond: workspace)
+    int32_t planecap;   // bitplane words in LDS (n * segcap / 64)
     int32_t r2lds;      // doubles of the r^2 tables copied to LDS (0: read from HBM / L2)
 };
-WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_total, int mask_words);
+// diff: one bit per sample pair (differ / not), for calc_nhaps
+WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_total, int mask_words, int segcap);
 
 struct StatsArgs {
     uint32_t stats;

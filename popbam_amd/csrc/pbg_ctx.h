@@ -74,6 +74,7 @@ struct pbg_ctx {
         const void *wins;
         uint32_t n_win, n_rows, stats;
         uint64_t zstride;   // ZnS list words per window at fixed places (0: pool)
+        int segcap;         // segregating rows per window kept in LDS (WinLds::segcap)
     };
     std::vector<Plan> plans;
     uint64_t *d_ws = nullptr, *d_wsoff = nullptr, *d_zns = nullptr;

@@ -78,6 +78,10 @@ __device__ __forceinline__ int wave_sum(int v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+__device__ __forceinline__ int wave_min(int v) {
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
 
 // Row r (0 .. 16/RB - 1) of a 16-byte word of RB-byte rows (include/popbam_gpu.h row format).
 template <int RB>
@@ -103,7 +107,7 @@ __device__ __forceinline__ void row_in_word(const uint4 &q, int r, typename RowM
 
 }  // namespace
 
-WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_total, int mask_words) {
+WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_total, int mask_words, int segcap) {
     WinLds L{};
     uint32_t b = 0;
     auto take = [&](uint32_t bytes) {
@@ -112,12 +116,14 @@ WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_to
         return o;
     };
     const bool planes = stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE);
-    const bool diff = stats & (PBG_S_NUCDIV | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE);
-    L.seg = take(kSegCap * 8 * mask_words);
+    // calc_nhaps only asks whether two samples differ: one bit per pair
+    const bool zero = stats & (PBG_S_HAP_K | PBG_S_HAP_EHHS);
+    L.segcap = segcap;
+    L.seg = take((uint32_t)segcap * 8 * mask_words);
     L.var = take(0);
-    L.planecap = planes ? n * (kSegCap / 64) : 0;
+    L.planecap = planes ? n * (segcap / 64) : 0;
     L.plane = take((uint32_t)L.planecap * 8);
-    L.diff = take(diff ? (uint32_t)(n * n * 2) : 0);
+    L.diff = take(zero ? (uint32_t)((n * n + 63) / 64) * 8 : 0);
     L.acc = take((stats & (PBG_S_NUCDIV | PBG_S_HAP_DXY)) ? (uint32_t)(np * np * 4) : 0);
     L.amin = take((stats & PBG_S_HAP_DXY) ? (uint32_t)(np * np * 4) : 0);
     L.bins = take((stats & (PBG_S_SFS | PBG_S_DIV_POP | PBG_S_HAP_K | PBG_S_HAP_EHHS))
@@ -136,12 +142,17 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     using M = typename RowMask<RB>::T;
     constexpr uint64_t NW = sizeof(M) / 8;   // pool words per mask
     extern __shared__ __align__(16) unsigned char sm[];
-    const uint32_t w = blockIdx.x;
+    // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs, so block b
+    // runs on XCD b % 8; giving XCD x the contiguous windows [x * per, (x + 1) * per) keeps
+    // neighbouring (overlapping) windows on one L2, which then serves their shared rows once
+    const uint32_t per = (n_win + 7) / 8;
+    const uint32_t w = n_win >= 64 ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
     if (w >= n_win) return;
     const WinLds &L = A.lds;
+    const uint32_t segcap = (uint32_t)L.segcap;
     M *s_seg = reinterpret_cast<M *>(sm + L.seg);
     uint64_t *s_plane = reinterpret_cast<uint64_t *>(sm + L.plane);
-    uint16_t *s_diff = reinterpret_cast<uint16_t *>(sm + L.diff);
+    uint64_t *s_zero = reinterpret_cast<uint64_t *>(sm + L.diff);   // bit (v*n + u): samples v and u do not differ
     int32_t *s_acc = reinterpret_cast<int32_t *>(sm + L.acc);
     int32_t *s_amin = reinterpret_cast<int32_t *>(sm + L.amin);
     int32_t *s_bins = reinterpret_cast<int32_t *>(sm + L.bins);
@@ -157,7 +168,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     for (int i = lane; i < L.r2lds; i += 64) s_r2[i] = T.r2[i];
 
     // ---- pass over the rows: counted total, ordered compaction of the segregating rows (the
-    // first kSegCap into LDS)
+    // first segcap into LDS)
     constexpr int R = 16 / RB;
     const uint4 *rw = reinterpret_cast<const uint4 *>(rows);
     const int64_t c0 = wb / R, c1 = (we + R - 1) / R;
@@ -221,15 +232,14 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         return S;
     };
     int my_counted = 0;
-    const uint32_t S = compact(s_seg, (uint32_t)kSegCap, true, my_counted);
+    const uint32_t S = compact(s_seg, segcap, true, my_counted);
     const int num_sites = wave_sum(my_counted);
     const int nwords = S > 0 ? (int)((S + 63) / 64) : 1;
     const bool need_planes = (stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY |
                                        PBG_S_TREE)) != 0;
-    const bool need_diff = (stats & (PBG_S_NUCDIV | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY | PBG_S_TREE)) != 0;
     // pool slice (u64 words): [seg rows: S masks][bitplanes: n*nwords, when they outgrow LDS]
     // [omega / Wall lists: np*S masks]
-    const bool over = S > (uint32_t)kSegCap;
+    const bool over = S > segcap;
     M *wsg = nullptr;
     uint64_t *wpl = nullptr;
     if (over || ld_ws) {
@@ -256,13 +266,13 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         __syncthreads();
         if (over) {
             int unused = 0;
-            (void)compact(wsg, S, false, unused);   // second pass, only for windows beyond kSegCap
+            (void)compact(wsg, S, false, unused);   // second pass, only for windows beyond segcap
         } else {
             for (uint32_t j = (uint32_t)lane; j < S; j += 64) wsg[j] = s_seg[j];
         }
     }
     __syncthreads();
-    auto seg_at = [&](uint32_t j) -> M { return j < (uint32_t)kSegCap ? s_seg[j] : wsg[j]; };
+    auto seg_at = [&](uint32_t j) -> M { return j < segcap ? s_seg[j] : wsg[j]; };
 
     const pbg_window_out &O = A.out;
     if (lane == 0) {
@@ -287,36 +297,55 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         }
         __syncthreads();
     }
-    if (need_diff) {   // calc_diff_matrix: u16 accumulation (wraps, Appendix A.7)
-        for (int pr = lane; pr < n * n; pr += 64) {
-            const int v = pr / n, u = pr - v * n;
-            uint32_t d = 0;
-            if (v != u)
-                for (int k = 0; k < nwords; ++k) d += pc(plane[v * nwords + k] ^ plane[u * nwords + k]);
-            s_diff[pr] = (uint16_t)(d & 0xFFFF);
+    // calc_diff_matrix (pop_nucdiv.cpp:242-256): u16 accumulation of XOR popcounts (wraps,
+    // Appendix A.7), computed pair by pair from the bitplanes and reduced on the spot:
+    //  - calc_nucdiv / calc_minDxy: pair (v, u), v < u, adds to (pop(v), pop(u)) when pop(v) <=
+    //    pop(u) -- the reference's i <= j loops (Dxy asymmetry, Appendix A.6).  Integer sums, exact
+    //    as the reference's doubles are: per pair of populations, lanes over its sample pairs, a
+    //    wave sum (and minimum);
+    //  - calc_nhaps: one bit per pair (the samples do not differ), from wave ballots.
+    auto pair_diff = [&](int v, int u) -> uint32_t {
+        uint32_t d = 0;
+        if (v != u)
+            for (int k = 0; k < nwords; ++k) d += pc(plane[v * nwords + k] ^ plane[u * nwords + k]);
+        return d & 0xFFFFu;
+    };
+    const bool sums = (stats & (PBG_S_NUCDIV | PBG_S_HAP_DXY)) != 0;
+    const bool zbits = (stats & (PBG_S_HAP_K | PBG_S_HAP_EHHS)) != 0;
+    if (zbits) {   // calc_nhaps: bit (v*n + u) = samples v and u do not differ
+        const int nn2 = n * n;
+        for (int pr0 = 0; pr0 < nn2; pr0 += 64) {
+            const int pr = pr0 + lane;
+            const int v = pr < nn2 ? pr / n : 0, u = pr < nn2 ? pr - v * n : 0;
+            const uint64_t m = __ballot(pr < nn2 && pair_diff(v, u) == 0);
+            if (lane == 0) s_zero[pr0 >> 6] = m;
         }
-        __syncthreads();
     }
-
-    // ---- pairwise-difference sums per population pair (calc_nucdiv / calc_minDxy): pair (v, u),
-    // v < u, adds to (pop(v), pop(u)) when pop(v) <= pop(u) -- the reference's i <= j loops
-    // (Dxy asymmetry, Appendix A.6).  Integer sums, exact as the reference's doubles are.
-    if (stats & (PBG_S_NUCDIV | PBG_S_HAP_DXY)) {
-        for (int i = lane; i < np * np; i += 64) {
-            s_acc[i] = 0;
-            if (stats & PBG_S_HAP_DXY) s_amin[i] = 65535;   // UINT_MAX narrowed to u16 (A.7)
-        }
-        __syncthreads();
-        for (int pr = lane; pr < n * n; pr += 64) {
-            const int v = pr / n, u = pr - v * n;
-            const int a = P.sample_pop[v], b = P.sample_pop[u];
-            if (v < u && a >= 0 && b >= 0 && a <= b) {
-                const int d = s_diff[pr];
-                atomicAdd(&s_acc[a * np + b], d);
-                if ((stats & PBG_S_HAP_DXY) && a < b) atomicMin(&s_amin[a * np + b], d);
+    if (sums) {   // per population pair (a, b), a <= b: lanes over its sample pairs (v, u), v < u
+        for (int a = 0; a < np; ++a)
+            for (int b = a; b < np; ++b) {
+                const int a0 = P.pop_start[a], na = P.pop_start[a + 1] - a0;
+                const int b0 = P.pop_start[b], nb = P.pop_start[b + 1] - b0;
+                int acc = 0, mn = 65535;   // UINT_MAX narrowed to u16 (A.7)
+                for (int q = lane; q < na * nb; q += 64) {
+                    const int x = q / nb, y = q - x * nb;
+                    const int v = P.pop_member[a0 + x], u = P.pop_member[b0 + y];
+                    if (v < u) {
+                        const int d = (int)pair_diff(v, u);
+                        acc += d;
+                        mn = min(mn, d);
+                    }
+                }
+                acc = wave_sum(acc);
+                if ((stats & PBG_S_HAP_DXY) && a < b) mn = wave_min(mn);
+                if (lane == 0) {
+                    s_acc[a * np + b] = acc;
+                    if (stats & PBG_S_HAP_DXY) s_amin[a * np + b] = a < b ? mn : 65535;
+                }
             }
-        }
-        __syncthreads();
+    }
+    if (sums || zbits) __syncthreads();
+    if (sums) {
         for (int pr = lane; pr < np * np; pr += 64) {
             const int i = pr / np, j = pr - i * np;
             if (j < i) continue;
@@ -533,7 +562,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                 for (int k = 0; k < nwords; ++k) d += pc(plane[smp * nwords + k]);
                 v = (int32_t)(d & 0xFFFF);
             } else if (a != b) {
-                v = s_diff[(a - 1) * n + (b - 1)];
+                v = (int32_t)pair_diff(a - 1, b - 1);
             }
             td[pr] = v;
         }
@@ -565,7 +594,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                 for (int j = 0; j < nelem - 1; j++) {
                     const int bj = b[j];
                     for (int k = j + 1 + lane; k < nelem; k += 64)
-                        if (s_diff[j * n + k] == 0 && b[k] > bj) b[k] = j;
+                        if (((s_zero[(j * n + k) >> 6] >> ((j * n + k) & 63)) & 1u) && b[k] > bj) b[k] = j;
                     __syncthreads();
                 }
                 // f_j = #{q : b[q] == j}, j < nelem: an LDS histogram
@@ -968,7 +997,8 @@ template __global__ void window_stats_kernel<16>(DevParams, DevTables, const voi
 hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, const void *rows, uint32_t n_rows,
                                uint32_t n_win, const StatsArgs &A, hipStream_t stream, int n_cu) {
     if (n_win == 0) return hipSuccess;
-    const dim3 g(n_win), b(64);
+    // window_stats_kernel's XCD-aware order: 8 * ceil(n_win / 8) workgroups (the extra exit at once)
+    const dim3 g(n_win >= 64 ? (n_win + 7) / 8 * 8 : n_win), b(64);
     const size_t lds = A.lds.bytes;
     switch (rb) {
         case 2: hipLaunchKernelGGL(window_stats_kernel<2>, g, b, lds, stream, P, T, rows, n_rows, n_win, A); break;

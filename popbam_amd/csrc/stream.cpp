@@ -113,6 +113,7 @@ int ensure_slot(pbg_ctx *c, pbg::StreamSlot &s, uint32_t chunk, size_t keys) {
         HIPCHK(c, hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&s.ev_free, hipEventDisableTiming));
     }
+    keys = std::max<size_t>(keys, 64);   // a chunk without keys still hands the kernels a keys pointer
     const bool need_pos = s.pos_cap < chunk;
     const bool need_keys = s.keys_cap < keys;
     if (!need_pos && !need_keys) return PBG_OK;

@@ -15,7 +15,8 @@ LIB_PATH = os.path.join(HERE, "libpopbam_feed.so")
 
 EXPORTS = ["pbf_last_error", "pbf_open", "pbf_close", "pbf_header_text", "pbf_n_refs", "pbf_ref_name",
            "pbf_ref_len", "pbf_has_index", "pbf_pileup", "pbf_pileup_mt", "pbf_batch_free", "pbf_fasta_fetch", "pbf_free",
-           "pbf_pack", "pbf_keys_free", "pbf_pileup_keys_mt"]
+           "pbf_pack", "pbf_keys_free", "pbf_pileup_keys_mt", "pbf_kstream_open", "pbf_kstream_next",
+           "pbf_kstream_profile", "pbf_kstream_close"]
 
 PBF_E_RG = -4
 
@@ -30,6 +31,16 @@ class PbfKeys(C.Structure):
     _fields_ = [("n_sites", C.c_uint32), ("pos0", C.c_int32), ("ref", C.POINTER(C.c_uint8)), ("k", C.c_void_p),
                 ("rmsq", C.POINTER(C.c_uint32)), ("block_off", C.POINTER(C.c_uint64)),
                 ("keys", C.POINTER(C.c_uint16)), ("n_keys", C.c_uint64)]
+
+
+class PbfProfile(C.Structure):
+    _fields_ = [("t_wall", C.c_double), ("t_fetch", C.c_double), ("t_inflate", C.c_double), ("t_walk", C.c_double),
+                ("t_consumer_wait", C.c_double), ("bytes_compressed", C.c_uint64), ("bytes_inflated", C.c_uint64),
+                ("records", C.c_uint64), ("threads", C.c_uint32), ("pieces", C.c_uint32),
+                ("crowded_pieces", C.c_uint32), ("_pad", C.c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "_pad"}
 
 
 class PbfFilter(C.Structure):
@@ -83,6 +94,13 @@ def load():
                                        C.c_char_p,
                                        P(C.c_char_p), P(C.c_int32), C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfFilter),
                                        P(PbfKeys)]
+    lib.pbf_kstream_open.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int, C.c_int32, C.c_int32, C.c_int32,
+                                     C.c_char_p, P(C.c_char_p), P(C.c_int32), C.c_int, C.c_int32, C.c_int, C.c_int,
+                                     P(PbfFilter), P(vp)]
+    lib.pbf_kstream_next.argtypes = [vp, P(PbfKeys)]
+    lib.pbf_kstream_profile.argtypes = [vp, P(PbfProfile)]
+    lib.pbf_kstream_close.argtypes = [vp]
+    lib.pbf_kstream_close.restype = None
     lib.pbf_fasta_fetch.argtypes = [C.c_char_p, C.c_char_p, P(C.c_void_p), P(C.c_int64)]
     lib.pbf_free.argtypes = [vp]
     lib.pbf_free.restype = None
@@ -109,7 +127,7 @@ def fasta_fetch(path: str, name: str) -> bytes:
 
 def _take_keys(lib, out: PbfKeys, n_samples: int, kb: int) -> dict:
     try:
-        L = out.n_sites
+        L, pos0 = out.n_sites, out.pos0
         ref = np.ctypeslib.as_array(out.ref, (max(L, 1),))[:L].copy()
         kt = C.c_uint8 if kb == 1 else C.c_uint16
         k = np.ctypeslib.as_array(C.cast(out.k, C.POINTER(kt)), (max(L * n_samples, 1),))[:L * n_samples].copy()
@@ -119,7 +137,7 @@ def _take_keys(lib, out: PbfKeys, n_samples: int, kb: int) -> dict:
     finally:
         lib.pbf_keys_free(C.byref(out))
     return {"ref": ref, "k": k.reshape(L, n_samples), "rmsq": rmsq.reshape(L, n_samples), "keys": keys,
-            "block_off": boff, "pos0": out.pos0}
+            "block_off": boff, "pos0": pos0}
 
 
 def pack(batch: dict, n_samples: int, flt: PbfFilter) -> dict:
@@ -207,10 +225,65 @@ class Bam:
                                                      C.byref(flt), C.byref(out)))
         return _take_keys(self.lib, out, n_samples, flt.k_bytes)
 
+    def key_stream(self, tid: int, beg: int, end: int, refseq: bytes, rg2s: dict, n_samples: int, max_depth: int,
+                   flt: PbfFilter, fallback_sample: int = -1, threads: int = 1, chunk: int = 1 << 20,
+                   win: int = 0) -> "KeyStream":
+        """pbf_kstream_*: the key batch of [beg, end) as pieces in position order, walked ahead by
+        `threads` workers."""
+        return KeyStream(self, tid, beg, end, refseq, rg2s, n_samples, max_depth, flt, fallback_sample, threads,
+                         chunk, win)
+
     def close(self):
         if self.h:
             self.lib.pbf_close(self.h)
             self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class KeyStream:
+    """Iterates the pieces (PbfKeys, library-owned: `release` each) of a region's key batch."""
+
+    def __init__(self, bam: Bam, tid, beg, end, refseq, rg2s, n_samples, max_depth, flt, fallback_sample, threads,
+                 chunk, win):
+        self.lib = bam.lib
+        if len(refseq) < end:
+            raise FeedError(-3, "reference sequence shorter than the region")
+        ids = list(rg2s)
+        self._keep = (refseq, (C.c_char_p * max(1, len(ids)))(*[i.encode() for i in ids]),
+                      (C.c_int32 * max(1, len(ids)))(*[rg2s[i] for i in ids]), flt)
+        self.h = C.c_void_p()
+        _check(self.lib, self.lib.pbf_kstream_open(bam.path.encode(), max(1, threads), chunk, tid, beg, end, win, refseq,
+                                                   self._keep[1], self._keep[2], len(ids), fallback_sample, n_samples,
+                                                   max_depth, C.byref(flt), C.byref(self.h)))
+
+    def next(self) -> PbfKeys | None:
+        p = PbfKeys()
+        r = _check(self.lib, self.lib.pbf_kstream_next(self.h, C.byref(p)))
+        return p if r == 1 else None
+
+    def release(self, p: PbfKeys):
+        self.lib.pbf_keys_free(C.byref(p))
+
+    def profile(self) -> dict:
+        pr = PbfProfile()
+        _check(self.lib, self.lib.pbf_kstream_profile(self.h, C.byref(pr)))
+        return pr.as_dict()
+
+    def close(self):
+        if self.h:
+            self.lib.pbf_kstream_close(self.h)
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
     def __del__(self):
         try:

@@ -31,34 +31,21 @@ def available() -> bool:
 
 
 def make_inputs(d: str, seed: int, L: int, n: int, npops: int = 2, read_len: int = 100, step: int = 10) -> str:
-    """ref.fa / in.bam / in.bam.bai of positions [0, L) of contig 0 of the synthetic genome."""
+    """ref.fa / in.bam / in.bam.bai of positions [0, L) of contig 0 of the synthetic genome
+    (oracle/synth_bam.cpp: the genotypes behind the benchmark's pileup, 100 bp reads every 10 bp
+    per sample, baseQ 40, mapQ 60, BGZF members compressed on several threads)."""
     import harness
-    from bamwriter import Read, write_bam, write_fasta
     os.makedirs(d, exist_ok=True)
     if os.path.exists(os.path.join(d, "in.bam.bai")):
         return d
     lib = harness.oracle()
-    lib.orc_synth_genotypes.restype = None
-    lib.orc_synth_genotypes.argtypes = [C.c_uint64, C.c_int32, C.c_uint64, C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p]
-    ref = np.zeros(L, np.uint8)
-    al = np.zeros((L, n), np.uint8)
-    lib.orc_synth_genotypes(seed, 0, 0, L, n, ref.ctypes.data, al.ctypes.data)
-    refseq = ref.tobytes().decode()
-    bases = np.frombuffer(b"ACGT", np.uint8)
-    per = n // npops
-    header = ["@HD\tVN:1.0\tSO:coordinate", f"@SQ\tSN:chr1\tLN:{L}"]
-    for s in range(n):
-        header.append(f"@RG\tID:rg{s}\tSM:s{s}\tPO:pop{min(s // per, npops - 1)}")
-    reads = []
-    for s in range(n):
-        for i, p in enumerate(range(s % step, L - read_len + 1, step)):
-            h = (i + s) & 1
-            seq = bases[(al[p:p + read_len, s] >> (2 * h)) & 3].tobytes().decode()
-            reads.append(Read(name=f"r{s}_{i}", tid=0, pos=p, mapq=60, flag=16 if (i >> 1) & 1 else 0,
-                              cigar=[("M", read_len)], seq=seq, qual=[40] * read_len, tags={"RG": f"rg{s}"}))
-    reads.sort(key=lambda r: r.pos)
-    write_fasta(os.path.join(d, "ref.fa"), [("chr1", refseq)])
-    write_bam(os.path.join(d, "in.bam"), "\n".join(header) + "\n", [("chr1", L)], reads)
+    lib.orc_write_synth_bam.restype = C.c_int
+    lib.orc_write_synth_bam.argtypes = [C.c_char_p, C.c_uint64, C.c_uint32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                        C.c_int32]
+    threads = max(1, min(16, os.cpu_count() or 1))
+    rc = lib.orc_write_synth_bam(d.encode(), seed, L, n, npops, read_len, step, threads)
+    if rc != 0:
+        raise RuntimeError(f"orc_write_synth_bam failed ({rc})")
     return d
 
 
@@ -69,25 +56,32 @@ def _run(d: str, cmd: str, region: str, win_kb: int) -> float:
     return time.perf_counter() - t0
 
 
-def time_reference(d: str, L: int, win: int, procs: int = 1) -> dict:
-    """Wall seconds of `popbam nucdiv|sfs|ld -w` over [0, L): one process per command, and
-    `procs` concurrent region-sharded processes per command (whole windows per shard)."""
+def time_reference(d: str, L: int, win: int, procs: int = 1, single: bool = True, capture: bool = False) -> dict:
+    """Wall seconds of `popbam nucdiv|sfs|ld -w` over [0, L): one process per command (single),
+    and `procs` concurrent region-sharded processes per command (whole windows per shard; with
+    capture, their stdout concatenated in shard order = the command's text)."""
     win_kb = win // 1000
-    one = {c: _run(d, c, "chr1", win_kb) for c in ("nucdiv", "sfs", "ld")}
-    out = {"single": one, "single_total_s": sum(one.values())}
+    out = {}
+    if single:
+        one = {c: _run(d, c, "chr1", win_kb) for c in ("nucdiv", "sfs", "ld")}
+        out.update({"single": one, "single_total_s": sum(one.values())})
     if procs > 1:
         nw = (L - 1) // win
         per = -(-nw // procs)
         regions = [f"chr1:{a * win + 1}-{min(nw, a + per) * win + 1}" for a in range(0, nw, per)]
-        par = {}
+        par, texts = {}, {}
         for c in ("nucdiv", "sfs", "ld"):
             t0 = time.perf_counter()
             ps = [subprocess.Popen([REF_BIN, c, "-f", "ref.fa", "-w", str(win_kb), "in.bam", r], cwd=d,
-                                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL) for r in regions]
-            for p in ps:
-                p.wait()
+                                   stdout=subprocess.PIPE if capture else subprocess.DEVNULL,
+                                   stderr=subprocess.DEVNULL) for r in regions]
+            outs = [p.communicate()[0] if capture else p.wait() for p in ps]
             par[c] = time.perf_counter() - t0
+            if capture:
+                texts[c] = b"".join(outs).decode()
         out["parallel"] = par
         out["parallel_total_s"] = sum(par.values())
         out["procs"] = len(regions)
+        if capture:
+            out["texts"] = texts
     return out

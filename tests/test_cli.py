@@ -141,6 +141,27 @@ def _main(argv, capsys):
     return rc, out.out, out.err
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,idx", [c for c in CASES if c[0] in ("g01_base", "g08_filters", "g10_deep", "g13_snpformats",
+                                                                  "g16_24s2p") and c[1] < 3])
+def test_cli_small_feeder_pieces_match_reference(gpu_lib, name, idx, monkeypatch):
+    """64-position feeder pieces on 3 worker threads: every piece is its own pbg_stream_push (two
+    device slots alternating, keys pointers shifted per chunk), and stdout is still the
+    reference's byte for byte."""
+    monkeypatch.setenv("POPBAM_FEED_CHUNK", "64")
+    monkeypatch.setenv("POPBAM_FEED_THREADS", "3")
+    cs = fixtures.load_case(name)["meta"]["cases"][idx]
+    argv = _argv(name, cs)
+    ours = cli.run(argv[0], argv[1:])
+    oob = None
+    if cs["args"][0] == "snp":
+        st = harness.Setup(name, cs["args"], cs["region"])
+        oob = harness.snp_oob_cells(harness.oracle_run(st))
+    ok, diff = harness.same_output(cs["args"], fixtures.golden_text(name, cs["stdout"]), ours, oob)
+    assert ok, f"{argv}\n gold: {diff[0]}\n ours: {diff[1]}"
+    assert cli.last_profile["gpu"]["pieces"] >= 1
+
+
 def test_usage_and_unknown_commands(capsys):
     rc, out, err = _main([], capsys)
     assert rc == 1 and "Usage:" in err and out == ""

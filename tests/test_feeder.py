@@ -222,3 +222,147 @@ def test_crowded_pileup_follows_the_reference_walks(tmp_path):
             assert np.array_equal(got["reads"], want["reads"]), (win, threads, chunk)
     assert len(seen) > 1   # the fixture does reach maxcnt differently per walk start
     bam.close()
+
+
+def test_crowded_key_batches_follow_the_reference_walks(tmp_path):
+    """The key path (pbf_pileup_keys_mt / pbf_kstream_*: records parsed into an arena, one walk
+    per piece) falls back to the reference's window-by-window walks where a read can meet a full
+    buffer (maxcnt): its keys equal pbf_pack of the raw reference walks for every window size."""
+    path, seq, rg2s = _crowded_bam(tmp_path)
+    bam = feed.Bam(path)
+    beg, end, X = 0, 320, 20000
+    flt = feed.make_filter(13, 13, 0, X)
+    for win in (0, 64, 37):
+        raw = bam.pileup(0, beg, end, seq, rg2s, 2, X, -1, threads=2, chunk=64, win=win)
+        want = feed.pack(raw, 2, flt)
+        for threads, chunk in [(1, 64), (3, 128), (2, 1 << 20)]:
+            got = bam.pileup_keys(0, beg, end, seq, rg2s, 2, X, flt, -1, threads=threads, chunk=chunk, win=win)
+            for f in ("ref", "k", "rmsq", "keys", "block_off"):
+                assert np.array_equal(got[f], want[f]), (win, threads, chunk, f)
+    bam.close()
+
+
+def test_key_stream_pieces_concatenate_to_the_batch():
+    """pbf_kstream_next hands out the pieces in position order; concatenated they are the
+    merged batch (pbf_pileup_keys_mt), and the profile counts the inflated bytes and records."""
+    c = fixtures.load_case("g16_24s2p")
+    bam = feed.Bam(os.path.join(c["dir"], "in.bam"))
+    seq = feed.fasta_fetch(os.path.join(c["dir"], "ref.fa"), bam.refs[0][0])
+    sm = opt.parse_header(bam.header_text, "in.bam")
+    flt = feed.make_filter(13, 13, 0, 255)
+    beg, end = 100, len(seq) - 3
+    whole = bam.pileup_keys(0, beg, end, seq, sm.rg2sample, sm.n, 255, flt, -1, threads=3, chunk=1000)
+    parts = []
+    with bam.key_stream(0, beg, end, seq, sm.rg2sample, sm.n, 255, flt, -1, threads=4, chunk=640) as ks:
+        while True:
+            p = ks.next()
+            if p is None:
+                break
+            parts.append(feed._take_keys(bam.lib, p, sm.n, 1))
+        prof = ks.profile()
+    assert [p["pos0"] for p in parts] == list(range(beg, end, 640))
+    assert np.array_equal(np.concatenate([p["keys"] for p in parts]), whole["keys"])
+    assert np.array_equal(np.concatenate([p["k"] for p in parts]), whole["k"])
+    assert np.array_equal(np.concatenate([p["ref"] for p in parts]), whole["ref"])
+    assert prof["pieces"] == len(parts) and prof["bytes_inflated"] > prof["bytes_compressed"] > 0
+    assert prof["records"] > 0 and prof["t_inflate"] <= prof["t_fetch"]
+    bam.close()
+
+
+def test_key_path_unknown_read_group_is_an_error():
+    c = fixtures.load_case("g01_base")
+    bam = feed.Bam(os.path.join(c["dir"], "in.bam"))
+    sm = opt.parse_header(bam.header_text, "in.bam")
+    rg2s = dict(list(sm.rg2sample.items())[1:])      # drop one read group
+    with pytest.raises(feed.FeedError) as e:
+        bam.pileup_keys(0, 0, 2000, c["refseq"], rg2s, sm.n, 255, feed.make_filter(13, 13, 0, 255), -1, threads=2,
+                        chunk=640)
+    assert e.value.code == feed.PBF_E_RG and "Problem assigning read group" in str(e.value)
+    bam.close()
+
+
+def test_zlib_and_libdeflate_inflate_alike(tmp_path):
+    """BGZF blocks inflate to the same records with libdeflate and with zlib's inflate (the
+    fallback, POPBAM_NO_LIBDEFLATE=1): the key batch is identical."""
+    import subprocess
+    import sys
+    code = ("import sys, numpy as np; sys.path[:0] = [%r, %r]; import fixtures, os\n"
+            "from popbam_amd import feed, options as opt\n"
+            "c = fixtures.load_case('g11_eleven'); bam = feed.Bam(os.path.join(c['dir'], 'in.bam'))\n"
+            "seq = feed.fasta_fetch(os.path.join(c['dir'], 'ref.fa'), bam.refs[0][0]); sm = opt.parse_header(bam.header_text, 'in.bam')\n"
+            "b = bam.pileup_keys(0, 0, len(seq), seq, sm.rg2sample, sm.n, 255, feed.make_filter(13, 13, 0, 255), -1, threads=2, chunk=4096)\n"
+            "np.save(sys.argv[1], b['keys'])\n") % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                    os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    outs = []
+    for env in ({}, {"POPBAM_NO_LIBDEFLATE": "1"}):
+        p = str(tmp_path / f"k{len(outs)}.npy")
+        subprocess.run([sys.executable, "-c", code, p], check=True, env=dict(os.environ, **env))
+        outs.append(np.load(p))
+    assert len(outs[0]) > 0 and np.array_equal(outs[0], outs[1])
+
+
+def _python_synth_bam(d, seed, L, n, npops=2, read_len=100, step=10):
+    """The record-by-record writer the native one (oracle/synth_bam.cpp) replaced: the same reads
+    through tests/golden/bamwriter.py."""
+    import ctypes as C
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import harness
+    from bamwriter import Read, write_bam, write_fasta
+    os.makedirs(d, exist_ok=True)
+    lib = harness.oracle()
+    lib.orc_synth_genotypes.restype = None
+    lib.orc_synth_genotypes.argtypes = [C.c_uint64, C.c_int32, C.c_uint64, C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p]
+    ref = np.zeros(L, np.uint8)
+    al = np.zeros((L, n), np.uint8)
+    lib.orc_synth_genotypes(seed, 0, 0, L, n, ref.ctypes.data, al.ctypes.data)
+    bases = np.frombuffer(b"ACGT", np.uint8)
+    per = n // npops
+    header = ["@HD\tVN:1.0\tSO:coordinate", f"@SQ\tSN:chr1\tLN:{L}"]
+    header += [f"@RG\tID:rg{s}\tSM:s{s}\tPO:pop{min(s // per, npops - 1)}" for s in range(n)]
+    reads = []
+    for s in range(n):
+        for i, p in enumerate(range(s % step, L - read_len + 1, step)):
+            h = (i + s) & 1
+            seq = bases[(al[p:p + read_len, s] >> (2 * h)) & 3].tobytes().decode()
+            reads.append(Read(name=f"r{s}_{i}", tid=0, pos=p, mapq=60, flag=16 if (i >> 1) & 1 else 0,
+                              cigar=[("M", read_len)], seq=seq, qual=[40] * read_len, tags={"RG": f"rg{s}"}))
+    reads.sort(key=lambda r: r.pos)
+    write_fasta(os.path.join(d, "ref.fa"), [("chr1", ref.tobytes().decode())])
+    write_bam(os.path.join(d, "in.bam"), "\n".join(header) + "\n", [("chr1", L)], reads)
+
+
+def test_native_synthetic_bam_equals_python_writer(tmp_path):
+    """oracle/synth_bam.cpp (the CPU baseline's and the command-line benchmark's BAM) holds the
+    same header, reference and reads as the Python writer's file, and POPBAM itself prints the
+    same text on both."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import ref_baseline
+    L, n = 30_000, 12
+    a, b = str(tmp_path / "native"), str(tmp_path / "python")
+    ref_baseline.make_inputs(a, 0xC0FFEE02, L, n)
+    _python_synth_bam(b, 0xC0FFEE02, L, n)
+    assert open(os.path.join(a, "ref.fa")).read() == open(os.path.join(b, "ref.fa")).read()
+    batches = []
+    for d in (a, b):
+        bam = feed.Bam(os.path.join(d, "in.bam"))
+        assert bam.has_index and bam.refs == [("chr1", L)]
+        sm = opt.parse_header(bam.header_text, "in.bam")
+        seq = feed.fasta_fetch(os.path.join(d, "ref.fa"), "chr1")
+        batches.append((bam.header_text, bam.pileup_keys(0, 0, L, seq, sm.rg2sample, sm.n, 255,
+                                                         feed.make_filter(13, 13, 0, 255), -1, threads=2, chunk=5000)))
+        # a region fetch through the index (linear index + bins)
+        part = bam.pileup_keys(0, 17_000, 23_000, seq, sm.rg2sample, sm.n, 255, feed.make_filter(13, 13, 0, 255), -1)
+        full = batches[-1][1]
+        lo, hi = int(full["k"][:17_000].sum()), int(full["k"][:23_000].sum())
+        assert np.array_equal(part["k"], full["k"][17_000:23_000]) and np.array_equal(part["keys"], full["keys"][lo:hi])
+        bam.close()
+    assert batches[0][0] == batches[1][0]
+    for f in ("ref", "k", "rmsq", "keys", "block_off"):
+        assert np.array_equal(batches[0][1][f], batches[1][1][f]), f
+    if ref_baseline.available():
+        outs = [subprocess.run([ref_baseline.REF_BIN, "nucdiv", "-f", "ref.fa", "-w", "5", "in.bam", "chr1:2001-27000"],
+                               cwd=d, capture_output=True, check=True).stdout for d in (a, b)]
+        assert outs[0] == outs[1] and outs[0].count(b"\n") >= 4

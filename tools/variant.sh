@@ -14,6 +14,7 @@ H=/opt/rocm/bin/hipcc
 $H $F --offload-arch=gfx950 -c -o $OUT/build/call.o $C/call_kernel.hip &
 $H $F --offload-arch=gfx950 -c -o $OUT/build/stats.o $C/stats_kernel.hip &
 $H $F -x hip --offload-arch=gfx950 -c -o $OUT/build/api.o $C/api.cpp &
+$H $F -x hip --offload-arch=gfx950 -c -o $OUT/build/stream.o $C/stream.cpp &
 $H $F -c -o $OUT/build/tables.o $C/host_tables.cpp &
 $H $F -c -o $OUT/build/format.o $C/format.cpp &
 wait || exit 1
