@@ -199,7 +199,7 @@ def cpu_baseline(args):
     if args.config == 4 or not ref_baseline.available():   # the reference cannot hold 96 samples
         return port
     L, n = args.ref_sample, args.samples
-    d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_v4_{args.seed:x}_{L}_{n}", args.seed, L, n)
+    d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_v5_{args.seed:x}_{L}_{n}", args.seed, L, n)
     procs = max(1, min(16, os.cpu_count() or 1))
     t = ref_baseline.time_reference(d, L, args.window, procs)
     out = {"value": round(L / t["single_total_s"] / 1e6, 6), "unit": "Msites/s", "cores": 1, "kind": "reference",
@@ -339,7 +339,7 @@ def cli_rate(args) -> dict:
     from popbam_amd import cli
     L, n = args.cli_sample, args.samples
     t0 = time.perf_counter()
-    d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_v4_{args.seed:x}_{L}_{n}", args.seed, L, n)
+    d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_v5_{args.seed:x}_{L}_{n}", args.seed, L, n)
     t_make = time.perf_counter() - t0
     win_kb = str(args.window // 1000)
     threads = int(os.environ.get("POPBAM_FEED_THREADS", min(16, os.cpu_count() or 1)))

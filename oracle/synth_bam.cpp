@@ -86,6 +86,13 @@ extern "C" int orc_write_synth_bam(const char *dir, uint64_t seed, uint32_t L, i
             fputc('\n', f);
         }
         fclose(f);
+        // ref.fa.fai (faidx: name, length, offset, bases per line, bytes per line), written here
+        // so that no reader builds it -- POPBAM's fai_load writes it on first use, which concurrent
+        // region-sharded processes would race on
+        FILE *fi = fopen((d + "/ref.fa.fai").c_str(), "wb");
+        if (!fi) return -2;
+        fprintf(fi, "chr1\t%u\t6\t60\t61\n", L);
+        fclose(fi);
     }
     // header block (records start on a fresh member, as samtools writes)
     std::string text = "@HD\tVN:1.0\tSO:coordinate\n@SQ\tSN:chr1\tLN:" + std::to_string(L) + "\n";
