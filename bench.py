@@ -524,6 +524,17 @@ def bench_genome(args, torch, dist, world, rank):
     ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
     scan_ms_alone = k1.value / max(1, n1.value)
     achieved_alone = sb0 / (scan_ms_alone * 1e-3) / 1e9
+    # the window statistics alone over the resident rows of the pass (HIP events on the call stream)
+    win_ms = None
+    if gp.stats:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        gp.stats_all()
+        e0.record(gp.call_stream)
+        for _ in range(3):
+            gp.stats_all()
+        e1.record(gp.call_stream)
+        gp.synchronize()
+        win_ms = e0.elapsed_time(e1) / 3
     pmc = pmc_traffic(args.config, {"contigs": args.contigs, "contig_len": args.contig_len, "samples": n,
                                     "depth": args.depth, "chunk": args.chunk, "world": world})
     traffic = pmc["kernels"]["call_scan_kernel"]["hbm_bytes"] if pmc else None
@@ -566,6 +577,11 @@ def bench_genome(args, torch, dist, world, rank):
             "call_stage": {"ms_per_pass": round(call_ms_pass, 3), "bytes_per_pass": sb,
                            "GBps": round(sb / (call_ms_pass * 1e-3) / 1e9, 2) if call_ms_pass else None,
                            "Msites_per_s_call_only": round(my_sites / (call_ms_pass * 1e-3) / 1e6, 2) if call_ms_pass else None},
+            "window_stage": ({"ms_per_pass": round(win_ms, 3), "windows": gp.n_windows,
+                              "row_bytes_per_pass": my_sites * ctx.row_bytes,
+                              "GBps_rows": round(my_sites * ctx.row_bytes / (win_ms * 1e-3) / 1e9, 2),
+                              "measured_on": "pbg_window_stats over the pass's resident rows, alone (3 passes, HIP "
+                                             "events on the call stream)"} if win_ms else None),
             "note": "value includes the on-device generation of every pileup chunk (the input does not fit "
                     "HBM: ~1.8 TB of keys); call_stage is the call kernels alone (library HIP events)",
             "pass_mode": "overlapped (two streams)" if args.overlap else "serial (generate, then call, per chunk)",

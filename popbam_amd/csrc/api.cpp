@@ -132,6 +132,17 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
                 if (d.sample_pop[v] == i) d.pop_member[at++] = (uint8_t)v;
         }
         for (int i = p->n_pops; i <= PBG_MAX_POPS; ++i) d.pop_start[i] = (int16_t)at;
+        d.pop_nmax = 0;
+        d.pops_ordered = 1;
+        int last = -1;   // largest member id of the populations so far
+        for (int i = 0; i < p->n_pops; ++i) {
+            const int a0 = d.pop_start[i], a1 = d.pop_start[i + 1];
+            d.pop_nmax = std::max(d.pop_nmax, a1 - a0);
+            if (a1 > a0) {
+                if (d.pop_member[a0] < last) d.pops_ordered = 0;
+                last = d.pop_member[a1 - 1];
+            }
+        }
     }
     for (int k = 0; k <= PBG_FAST_MAX; ++k) d.rms_thr[k] = rms_threshold(k, p->min_rmsQ, p->min_depth, p->max_depth);
     d.rmsq_thr[0] = p->min_rmsQ <= 0 ? 0u : 0xFFFFFFFFu;

@@ -27,6 +27,8 @@ struct DevParams {
     uint32_t flag;
     int32_t k16;          // k[] is u16 (max_depth > 255), else u8
     int32_t sfs_stride;   // largest population + 1 (pbg_window_out.sfs_bins row)
+    int32_t pop_nmax;     // members of the largest population (calc_nhaps' local indices stay below it)
+    int32_t pops_ordered; // every member of population a has a smaller id than every member of b > a
     int8_t sample_pop[PBG_MAX_SAMPLES];   // population of each sample (-1: none); masks are disjoint
     uint8_t pop_member[PBG_MAX_SAMPLES];  // the samples of population 0, then 1, ... (ascending within one)
     int16_t pop_start[PBG_MAX_POPS + 1];  // population i's samples: pop_member[pop_start[i], pop_start[i+1])

@@ -123,7 +123,7 @@ WinLds stats_lds_layout(int n, int np, int sfs_stride, uint32_t stats, int r2_to
     L.var = take(0);
     L.planecap = planes ? n * (segcap / 64) : 0;
     L.plane = take((uint32_t)L.planecap * 8);
-    L.diff = take(zero ? (uint32_t)((n * n + 63) / 64) * 8 : 0);
+    L.diff = take(zero ? (uint32_t)(n * ((n + 63) / 64)) * 8 : 0);   // row j: ceil(n / 64) words
     L.acc = take((stats & (PBG_S_NUCDIV | PBG_S_HAP_DXY)) ? (uint32_t)(np * np * 4) : 0);
     L.amin = take((stats & PBG_S_HAP_DXY) ? (uint32_t)(np * np * 4) : 0);
     L.bins = take((stats & (PBG_S_SFS | PBG_S_DIV_POP | PBG_S_HAP_K | PBG_S_HAP_EHHS))
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     const uint32_t segcap = (uint32_t)L.segcap;
     M *s_seg = reinterpret_cast<M *>(sm + L.seg);
     uint64_t *s_plane = reinterpret_cast<uint64_t *>(sm + L.plane);
-    uint64_t *s_zero = reinterpret_cast<uint64_t *>(sm + L.diff);   // bit (v*n + u): samples v and u do not differ
+    uint64_t *s_zero = reinterpret_cast<uint64_t *>(sm + L.diff);   // [v][u / 64] bit u % 64: v and u do not differ
     int32_t *s_acc = reinterpret_cast<int32_t *>(sm + L.acc);
     int32_t *s_amin = reinterpret_cast<int32_t *>(sm + L.amin);
     int32_t *s_bins = reinterpret_cast<int32_t *>(sm + L.bins);
@@ -235,8 +235,27 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     const uint32_t S = compact(s_seg, segcap, true, my_counted);
     const int num_sites = wave_sum(my_counted);
     const int nwords = S > 0 ? (int)((S + 63) / 64) : 1;
-    const bool need_planes = (stats & (PBG_S_NUCDIV | PBG_S_DIV_IND | PBG_S_HAP_K | PBG_S_HAP_EHHS | PBG_S_HAP_DXY |
-                                       PBG_S_TREE)) != 0;
+    const bool sums = (stats & (PBG_S_NUCDIV | PBG_S_HAP_DXY)) != 0;
+    const bool zbits = (stats & (PBG_S_HAP_K | PBG_S_HAP_EHHS)) != 0;
+    // calc_nucdiv's population-pair sums (below) come from per-site derived counts instead of
+    // sample pairs when no pair's u16 difference can wrap (S < 2^16), every pair v < u of the
+    // sums has pop(v) <= pop(u) (populations in id order), no minimum is asked for and it is the
+    // shorter loop
+    bool fast_sums = false;
+    if (sums && !(stats & PBG_S_HAP_DXY) && P.pops_ordered && S < 65536u) {
+        int cost_pairs = 0;
+        for (int a = 0; a < np; ++a)
+            for (int b = a; b < np; ++b) {
+                const int na = P.pop_start[a + 1] - P.pop_start[a], nb = P.pop_start[b + 1] - P.pop_start[b];
+                cost_pairs += (na * nb + 63) / 64;
+            }
+        fast_sums = np * (np + 1) / 2 * (int)((S + 63) / 64) <= cost_pairs * nwords;
+    }
+    // bitplanes: every sample's, or only calc_nhaps' (its local indices stay below pop_nmax)
+    const int plane_n = ((stats & (PBG_S_DIV_IND | PBG_S_HAP_DXY | PBG_S_TREE)) || ((stats & PBG_S_NUCDIV) && !fast_sums))
+                            ? n
+                            : (zbits ? min(n, P.pop_nmax) : 0);
+    const bool need_planes = plane_n > 0;
     // pool slice (u64 words): [seg rows: S masks][bitplanes: n*nwords, when they outgrow LDS]
     // [omega / Wall lists: np*S masks]
     const bool over = S > segcap;
@@ -286,13 +305,26 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
     uint64_t *plane = nullptr;
     if (need_planes) {
         plane = (n * nwords <= L.planecap) ? s_plane : wpl;
-        // plane[v*nwords + k] bit b = sample v derived at segregating site 64k+b (hap.seq)
-        for (int k = 0; k < nwords; ++k) {
-            const uint32_t j = (uint32_t)(k * 64 + lane);
-            const M t = j < S ? seg_at(j) : M{};
-            for (int v = 0; v < n; ++v) {
-                const uint64_t m = __ballot(bit(t, v));
-                if (lane == 0) plane[v * nwords + k] = m;
+        // plane[v*nwords + k] bit b = sample v derived at segregating site 64k+b (hap.seq), rows
+        // v < plane_n: one ballot per (word, sample), or, for few sites, lanes over the samples
+        // each gathering its bits from the (LDS) rows
+        if (nwords == 1 && (int)S * ((plane_n + 63) / 64) < plane_n) {
+            for (int v0 = 0; v0 < plane_n; v0 += 64) {
+                const int v = v0 + lane;
+                if (v < plane_n) {
+                    uint64_t m = 0;
+                    for (uint32_t j = 0; j < S; ++j) m |= (uint64_t)bit(s_seg[j], v) << j;
+                    plane[v] = m;
+                }
+            }
+        } else {
+            for (int k = 0; k < nwords; ++k) {
+                const uint32_t j = (uint32_t)(k * 64 + lane);
+                const M t = j < S ? seg_at(j) : M{};
+                for (int v = 0; v < plane_n; ++v) {
+                    const uint64_t m = __ballot(bit(t, v));
+                    if (lane == 0) plane[v * nwords + k] = m;
+                }
             }
         }
         __syncthreads();
@@ -310,18 +342,33 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
             for (int k = 0; k < nwords; ++k) d += pc(plane[v * nwords + k] ^ plane[u * nwords + k]);
         return d & 0xFFFFu;
     };
-    const bool sums = (stats & (PBG_S_NUCDIV | PBG_S_HAP_DXY)) != 0;
-    const bool zbits = (stats & (PBG_S_HAP_K | PBG_S_HAP_EHHS)) != 0;
-    if (zbits) {   // calc_nhaps: bit (v*n + u) = samples v and u do not differ
-        const int nn2 = n * n;
-        for (int pr0 = 0; pr0 < nn2; pr0 += 64) {
-            const int pr = pr0 + lane;
-            const int v = pr < nn2 ? pr / n : 0, u = pr < nn2 ? pr - v * n : 0;
-            const uint64_t m = __ballot(pr < nn2 && pair_diff(v, u) == 0);
-            if (lane == 0) s_zero[pr0 >> 6] = m;
-        }
+    const int zw = (n + 63) >> 6;   // s_zero words per row
+    if (zbits) {   // calc_nhaps: row v bit u (v < u < pop_nmax) = samples v and u do not differ
+        const int zn = min(n, P.pop_nmax);
+        for (int v = 0; v + 1 < zn; ++v)
+            for (int u0 = (v + 1) & ~63; u0 < zn; u0 += 64) {
+                const int u = u0 + lane;
+                const uint64_t m = __ballot(u > v && u < zn && pair_diff(v, u) == 0);
+                if (lane == 0) s_zero[v * zw + (u0 >> 6)] = m;
+            }
     }
-    if (sums) {   // per population pair (a, b), a <= b: lanes over its sample pairs (v, u), v < u
+    if (sums && fast_sums) {
+        // pair (a, b): sum over sites of c_a (n_b - c_b) + (n_a - c_a) c_b, a < b, or c_a (n_a - c_a)
+        // (c = derived members at the site): the same integers as the sample-pair loop below
+        for (int a = 0; a < np; ++a)
+            for (int b = a; b < np; ++b) {
+                const int na = P.pop_start[a + 1] - P.pop_start[a], nb = P.pop_start[b + 1] - P.pop_start[b];
+                const M ma = pop_mask<M>(P, a), mb = pop_mask<M>(P, b);
+                int acc = 0;
+                for (uint32_t j = (uint32_t)lane; j < S; j += 64) {
+                    const M t = seg_at(j);
+                    const int ca = (int)pc(t & ma), cb = (int)pc(t & mb);
+                    acc += a == b ? ca * (na - ca) : ca * (nb - cb) + (na - ca) * cb;
+                }
+                acc = wave_sum(acc);
+                if (lane == 0) s_acc[a * np + b] = acc;
+            }
+    } else if (sums) {   // per population pair (a, b), a <= b: lanes over its sample pairs (v, u), v < u
         for (int a = 0; a < np; ++a)
             for (int b = a; b < np; ++b) {
                 const int a0 = P.pop_start[a], na = P.pop_start[a + 1] - a0;
@@ -577,29 +624,35 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
             int32_t *b = s_bins + i * bstride;    // sample ids of the population (<= sfs_stride - 1)
             int32_t *hist = s_bins + np * bstride;   // scratch slice after the populations'
             if (nelem > 1) {
-                // b[c] = global id of the population's c-th sample (ordered compaction)
-                int base = 0;
-                for (int v0 = 0; v0 < n; v0 += 64) {
-                    const int v = v0 + lane;
-                    const bool in = v < n && P.sample_pop[v] == i;
-                    const uint64_t m = __ballot(in);
-                    if (in) b[base + (int)__popcll(m & ((1ULL << lane) - 1))] = v;
-                    base += (int)__popcll(m);
-                }
+                // b[c] = global id of the population's c-th sample (pop_member: ascending ids)
+                const int a0 = P.pop_start[i];
                 for (int j = lane; j < nelem; j += 64) hist[j] = 0;
-                __syncthreads();
                 // calc_nhaps's merge loop (pop_haplo.cpp:221-231), local indices j, k into the
                 // global diff matrix (A.11).  Step j only reads b[j], final once steps < j are
                 // done, and each b[k], k > j: the k's of one step run across lanes.
-                for (int j = 0; j < nelem - 1; j++) {
-                    const int bj = b[j];
-                    for (int k = j + 1 + lane; k < nelem; k += 64)
-                        if (((s_zero[(j * n + k) >> 6] >> ((j * n + k) & 63)) & 1u) && b[k] > bj) b[k] = j;
+                auto zero_bit = [&](int j, int k) -> bool { return (s_zero[j * zw + (k >> 6)] >> (k & 63)) & 1u; };
+                if (nelem <= 64) {   // b in registers: lane k holds b[k]
+                    int bk = lane < nelem ? (int)P.pop_member[a0 + lane] : 0;
+                    for (int j = 0; j < nelem - 1; j++) {
+                        const int bj = __builtin_amdgcn_readlane(bk, j);
+                        const uint64_t zrow = s_zero[j * zw];
+                        if (lane > j && lane < nelem && ((zrow >> lane) & 1u) && bk > bj) bk = j;
+                    }
                     __syncthreads();
+                    // f_j = #{q : b[q] == j}, j < nelem: an LDS histogram
+                    if (lane < nelem && bk >= 0 && bk < nelem) atomicAdd(&hist[bk], 1);
+                } else {
+                    for (int j = lane; j < nelem; j += 64) b[j] = (int)P.pop_member[a0 + j];
+                    __syncthreads();
+                    for (int j = 0; j < nelem - 1; j++) {
+                        const int bj = b[j];
+                        for (int k = j + 1 + lane; k < nelem; k += 64)
+                            if (zero_bit(j, k) && b[k] > bj) b[k] = j;
+                        __syncthreads();
+                    }
+                    for (int q = lane; q < nelem; q += 64)
+                        if (b[q] >= 0 && b[q] < nelem) atomicAdd(&hist[b[q]], 1);
                 }
-                // f_j = #{q : b[q] == j}, j < nelem: an LDS histogram
-                for (int q = lane; q < nelem; q += 64)
-                    if (b[q] >= 0 && b[q] < nelem) atomicAdd(&hist[b[q]], 1);
                 __syncthreads();
                 int my_nh = 0, my_ff = 0;
                 for (int j = lane; j < nelem; j += 64) {

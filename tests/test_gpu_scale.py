@@ -213,6 +213,46 @@ def test_window_stats_match_oracle(gpu_lib, n, npops, layout, stat, cmd_id, outp
     ctx.close()
 
 
+def _interleaved_params(n, npops):
+    """Populations dealt round-robin over the samples (sample v -> population v % npops), so
+    pairs v < u with pop(v) > pop(u) exist (the Dxy asymmetry, Appendix A.6)."""
+    from popbam_amd import workload
+    p = workload.default_params(n, npops)
+    masks = [0] * npops
+    for i in range(npops):
+        p.pop_n[i] = 0
+    for v in range(n):
+        masks[v % npops] |= 1 << v
+        p.pop_n[v % npops] += 1
+    for i, m in enumerate(masks):
+        p.set_pop_mask(i, m)
+    return p
+
+
+@pytest.mark.parametrize("n,npops,interleave", [(12, 2, True), (30, 3, True), (96, 3, True), (126, 2, True),
+                                                (96, 1, False), (126, 1, False), (70, 2, False)])
+@pytest.mark.parametrize("stat,cmd_id,output", [(0x001, 4, 0), (0x080, 1, 0), (0x100, 1, 1), (0x200, 1, 2),
+                                                (0x400, 3, 0)])
+def test_window_stats_population_layouts(gpu_lib, n, npops, interleave, stat, cmd_id, output):
+    """Population layouts beside the contiguous default: interleaved populations (calc_nucdiv's
+    sums then come from sample pairs, not per-site counts) and populations of more than 64
+    samples (calc_nhaps' merge in LDS instead of registers), on 1 kb / 500 bp windows (few
+    segregating sites: bitplanes gathered per sample) and 10 kb windows."""
+    import torch
+    from popbam_amd import _lib, workload
+    params = _interleaved_params(n, npops) if interleave else workload.default_params(n, npops)
+    ctx = _lib.Context(params, 0)
+    n_sites = 64 * 2000
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 3 * n)
+    wins = [(s, s + 1000) for s in range(0, n_sites - 1000, 500)] + workload.reference_windows(0, n_sites, 10_000)
+    hp = workload.HotPath(ctx, syn, wins, stat)
+    hp.step()
+    torch.cuda.synchronize()
+    types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites, n)
+    assert _window_text(ctx, params, hp, cmd_id, output, wins) == _oracle_text(params, types, flags, cmd_id, output, wins)
+    ctx.close()
+
+
 @pytest.mark.parametrize("n,npops", [(12, 2), (24, 3), (64, 4), (96, 3)])
 def test_u16_wrap_and_workspace_window(gpu_lib, n, npops):
     """One window over 1.28 M positions: ~25 k segregating sites (beyond LDS -> global
