@@ -610,7 +610,8 @@ def main():
         # gloo (host) for the timing barrier and the max over ranks: the data path has no
         # collective, so RCCL is never initialised
         import torch.distributed as dist
-        torch.cuda.set_device(local)
+        # one rank per GPU; more ranks than GPUs (a rehearsal on a smaller box) share them
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)

@@ -849,6 +849,12 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
 // two LDS reads (the row's entry a broadcast), five VALU and the table read.
 // Otherwise the raw masks (u64 / two-word) are read from the list buffer in HBM / L2, the table
 // from LDS or HBM.
+#ifndef PBG_ZNS_EXP
+#define PBG_ZNS_EXP 0   // timing experiments only (wrong results): 1 producers idle, 2 adder idle
+#endif
+#ifndef PBG_ZNS_PRIO
+#define PBG_ZNS_PRIO 3
+#endif
 constexpr int kZnsMaxC = 60;                 // chains per workgroup (64 + 16 C <= 1024 threads)
 constexpr int kZnsR = 8;                     // rounds per phase
 constexpr int kZnsRingStride = 18;           // doubles per (round, chain): 16 values + 2 pad (LDS banks)
@@ -944,6 +950,9 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
     __syncthreads();   // the staged lists
     if (tid < 64) {
         // ---- the adder: lane c sums chain c's values in pair order
+#if PBG_ZNS_PRIO
+        __builtin_amdgcn_s_setprio(PBG_ZNS_PRIO);   // the dependent chain issues ahead of the producers
+#endif
         double acc = 0.0;
         for (long long k = 0; k <= nphase; ++k) {   // phase k: sum phase k - 1 (the producers write phase k)
             if (k >= 1 && tid < C) {
@@ -959,11 +968,13 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
 #pragma unroll
                         for (int x = 0; x < 8; ++x) nv[x] = rg[(size_t)(r + 1) * (rstride / 2) + x];
                     }
+#if PBG_ZNS_EXP != 2   // (timing experiment 2: no adds)
 #pragma unroll
                     for (int x = 0; x < 8; ++x) {
                         acc += v[x].x;
                         acc += v[x].y;
                     }
+#endif
                     if (r + 1 < kZnsR) {
 #pragma unroll
                         for (int x = 0; x < 8; ++x) v[x] = nv[x];
@@ -990,7 +1001,7 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
     const M *L = reinterpret_cast<const M *>(z.list);
     const double *tab = r2_lds ? s_r2t : T.r2;
     for (long long k = 0; k <= nphase; ++k) {
-        if (k < nphase) {
+        if (k < nphase && PBG_ZNS_EXP != 1) {   // (timing experiment 1: producers idle)
             double *out = s_ring + (size_t)(k & 1) * kZnsR * rstride + (size_t)c * kZnsRingStride + j;
             // the phase's pairs first (pure VALU), then every load of the phase in flight at once
             int pa[kZnsR], pb[kZnsR];
