@@ -612,7 +612,15 @@ def main():
         import torch.distributed as dist
         # one rank per GPU; more ranks than GPUs (a rehearsal on a smaller box) share them
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-        dist.init_process_group("gloo")
+        # gloo announces its peer connections on stdout: keep them off the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     else:
         torch.cuda.set_device(0)
 

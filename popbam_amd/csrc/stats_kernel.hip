@@ -852,6 +852,9 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
 #ifndef PBG_ZNS_EXP
 #define PBG_ZNS_EXP 0   // timing experiments only (wrong results): 1 producers idle, 2 adder idle
 #endif
+#ifndef PBG_ZNS_SORT
+#define PBG_ZNS_SORT 1
+#endif
 #ifndef PBG_ZNS_PRIO
 #define PBG_ZNS_PRIO 3
 #endif
@@ -932,6 +935,22 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
         if (z.V > cap) atomicAnd(&s_fits, 0);
     }
     __syncthreads();
+    // producer group / adder lane g works on chain s_ord[g]: the workgroup's chains longest first,
+    // so the producer waves of the short ones (four consecutive groups each) run out together and
+    // skip their remaining phases
+    __shared__ int s_ord[kZnsMaxC];
+    if (tid < C) {
+        int rk = tid;
+        if (PBG_ZNS_SORT) {
+            const long long rt = zns_rounds(s_ch[tid].V);
+            rk = 0;
+            for (int c2 = 0; c2 < C; ++c2) {
+                const long long r2 = zns_rounds(s_ch[c2].V);
+                rk += (r2 > rt || (r2 == rt && c2 < tid)) ? 1 : 0;
+            }
+        }
+        s_ord[rk] = tid;
+    }
     const long long nphase = (s_rounds + kZnsR - 1) / kZnsR;
     const bool fast = s_fits != 0 && r2_lds != 0;   // workgroup-uniform
     if (fast) {   // stage the lists compacted: wave v takes chains v, v + (waves), ...
@@ -954,8 +973,11 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
         __builtin_amdgcn_s_setprio(PBG_ZNS_PRIO);   // the dependent chain issues ahead of the producers
 #endif
         double acc = 0.0;
+        const int cg = tid < C ? s_ord[tid] : 0;
+        const long long rg_end = tid < C ? zns_rounds(s_ch[cg].V) : 0;   // the chain's rounds
         for (long long k = 0; k <= nphase; ++k) {   // phase k: sum phase k - 1 (the producers write phase k)
-            if (k >= 1 && tid < C) {
+            // (a phase past the chain's last round holds only +0.0 or, skipped, nothing: no adds)
+            if (k >= 1 && tid < C && (k - 1) * kZnsR < rg_end) {
                 const double2 *rg = reinterpret_cast<const double2 *>(s_ring + (size_t)((k - 1) & 1) * kZnsR * rstride +
                                                                       (size_t)tid * kZnsRingStride);
                 double2 v[8];
@@ -983,17 +1005,18 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
             }
             __syncthreads();
         }
-        if (tid < C && ch0 + (uint32_t)tid < nch) {
-            const ZnsChain z = s_ch[tid];
+        if (tid < C && ch0 + (uint32_t)cg < nch) {
+            const ZnsChain z = s_ch[cg];
             double val = 0.0;
             if (A.seg_count[z.w] >= 1) val = acc * (2.0 / (z.ns * (z.ns - 1)));
-            if (A.out.ld_val) A.out.ld_val[ch0 + (uint32_t)tid] = x86nan(val);
+            if (A.out.ld_val) A.out.ld_val[ch0 + (uint32_t)cg] = x86nan(val);
         }
         return;
     }
     // ---- the producers: group c = (tid - 64) / 16 walks chain c, lane j takes pair (a, b0 + j)
-    const int p = tid - 64, j = p & 15, c = p >> 4;
+    const int p = tid - 64, j = p & 15, g = p >> 4, c = s_ord[g];
     const ZnsChain z = s_ch[c];
+    const long long my_rounds = zns_rounds(z.V);
     const int V = z.V, V1 = z.V - 1, np1 = z.np1, r2o = z.r2o, vm = max(V1, 0);
     int a = 0, b0 = 1;
     const uint32_t *lst = s_lst + c * cap;
@@ -1001,8 +1024,9 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
     const M *L = reinterpret_cast<const M *>(z.list);
     const double *tab = r2_lds ? s_r2t : T.r2;
     for (long long k = 0; k <= nphase; ++k) {
-        if (k < nphase && PBG_ZNS_EXP != 1) {   // (timing experiment 1: producers idle)
-            double *out = s_ring + (size_t)(k & 1) * kZnsR * rstride + (size_t)c * kZnsRingStride + j;
+        // (a wave whose four chains are all past their last round skips the phase)
+        if (k < nphase && PBG_ZNS_EXP != 1 && __ballot(k * kZnsR < my_rounds) != 0) {   // (exp 1: producers idle)
+            double *out = s_ring + (size_t)(k & 1) * kZnsR * rstride + (size_t)g * kZnsRingStride + j;
             // the phase's pairs first (pure VALU), then every load of the phase in flight at once
             int pa[kZnsR], pb[kZnsR];
             bool ok[kZnsR];
