@@ -457,6 +457,30 @@ def parity_sampled_genome(args, ctx, gp, k: int) -> dict:
     return r
 
 
+def rows_crosscheck(torch, ctx, hp) -> dict:
+    """Checker (outside the timed region), size-independent: the timed step's rows over the
+    whole batch against the consensus-word call of the same batch (pbg_call_sites with words:
+    call_sites_kernel runs errmod_cal + gl2cns on every task, none of the rows-only pipeline's
+    shortcuts -- the reference-only test, uniform_ref, one_error_ref and their bound margins).
+    Identical rows at every position are the full-size check of those shortcuts."""
+    t0 = time.perf_counter()
+    rows = hp.rows.clone()
+    n = ctx.params.n_samples
+    cb = torch.empty(hp.synth.n_sites * n, dtype=torch.int64, device="cuda")
+    hp.call(cb=cb)
+    torch.cuda.synchronize()
+    ctx.sync_check()
+    rb = ctx.row_bytes
+    a, b = rows.view(-1, rb), hp.rows.view(-1, rb)
+    ndiff = int((a != b).any(dim=1).sum().item())
+    del cb
+    hp.call()   # the rows-only rows back in place
+    torch.cuda.synchronize()
+    return {"identical": ndiff == 0, "positions": hp.synth.n_sites, "positions_differing": ndiff,
+            "paths": "rows-only pipeline (scan shortcuts + queues) vs consensus-word call (full errmod per task)",
+            "seconds": round(time.perf_counter() - t0, 2)}
+
+
 def max_over_ranks(dist, x: float) -> float:
     """The slowest rank's time (gloo, on the host)."""
     if not dist:
@@ -750,6 +774,7 @@ def main():
             ps = parity_sampled_resident(args, ctx, hp, wins, rank)
             out["parity_sampled"] = ps["ok"]
             out["parity_sample"] = ps
+            out["rows_crosscheck"] = rows_crosscheck(torch, ctx, hp)
         out["src_sha"] = source_hash()
         print(json.dumps(out), flush=True)
     ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")

@@ -126,6 +126,30 @@ def test_rows_only_call_matches_oracle(gpu_lib, n, kw):
     ctx.close()
 
 
+@pytest.mark.parametrize("n,kw,n_sites", [(12, {}, 64 * 60000), (24, {"flag": 0x02}, 64 * 20000),
+                                           (96, {}, 64 * 6000), (12, {"min_snpQ": 40}, 64 * 20000)])
+def test_rows_only_equals_consensus_word_call(gpu_lib, n, kw, n_sites):
+    """Size-independent check of the rows-only pipeline's shortcuts (the reference-only test,
+    uniform_ref, one_error_ref and their bound margins): over every position of a batch far
+    larger than the oracle cases, its rows equal those of the consensus-word call, which runs
+    errmod_cal + gl2cns on every task (bench.py's rows_crosscheck does the same at 50 Msites)."""
+    import torch
+    from popbam_amd import workload
+    ctx, params = _ctx(n, **kw)
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 11 * n)
+    hp = workload.HotPath(ctx, syn, [(0, n_sites)], 0)
+    hp.call()
+    ctx.sync_check()
+    fast = hp.rows.clone()
+    cb = torch.zeros(n_sites * n, dtype=torch.int64, device="cuda")
+    hp.call(cb=cb)
+    ctx.sync_check()
+    rb = ctx.row_bytes
+    bad = torch.nonzero((fast.view(-1, rb) != hp.rows.view(-1, rb)).any(dim=1)).flatten()
+    assert bad.numel() == 0, f"{bad.numel()} rows differ, first at {int(bad[0])}"
+    ctx.close()
+
+
 def _window_text(ctx, params, hp, cmd_id, output, windows, min_freq=1, jc=0, min_snps=10, flag_sub=False):
     """Format the GPU window outputs with the library's print_<stat> (pbg_format)."""
     from popbam_amd import _lib
