@@ -481,6 +481,30 @@ def rows_crosscheck(torch, ctx, hp) -> dict:
             "seconds": round(time.perf_counter() - t0, 2)}
 
 
+def genome_rows_crosscheck(torch, ctx, gp, slot: int = 0) -> dict:
+    """rows_crosscheck on one streamed chunk (chunk 0, generated into `slot`): the rows-only
+    call and the consensus-word call of its whole batch, into scratch rows."""
+    from popbam_amd import _lib
+    t0 = time.perf_counter()
+    si, p, L = gp.chunks[0]
+    b = gp.buf[slot]
+    pl = _lib.PbgPileup(L, p, b["ref"].data_ptr(), b["k"].data_ptr(), b["rmsq"].data_ptr(), b["block_off"].data_ptr(),
+                        b["keys"].data_ptr())
+    rb, n = ctx.row_bytes, ctx.params.n_samples
+    fast = torch.zeros(L * rb, dtype=torch.uint8, device="cuda")
+    full = torch.zeros_like(fast)
+    cb = torch.empty(L * n, dtype=torch.int64, device="cuda")
+    st = gp.call_stream.cuda_stream
+    ctx.check(ctx.lib.pbg_call_sites(ctx.h, C.byref(pl), fast.data_ptr(), None, st), "pbg_call_sites")
+    ctx.check(ctx.lib.pbg_call_sites(ctx.h, C.byref(pl), full.data_ptr(), cb.data_ptr(), st), "pbg_call_sites")
+    gp.synchronize()
+    ndiff = int((fast.view(-1, rb) != full.view(-1, rb)).any(dim=1).sum().item())
+    del cb, fast, full
+    return {"identical": ndiff == 0, "positions": L, "positions_differing": ndiff,
+            "paths": "rows-only pipeline vs consensus-word call, chunk 0 of the pass",
+            "seconds": round(time.perf_counter() - t0, 2)}
+
+
 def max_over_ranks(dist, x: float) -> float:
     """The slowest rank's time (gloo, on the host)."""
     if not dist:
@@ -548,6 +572,7 @@ def bench_genome(args, torch, dist, world, rank):
     ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
     scan_ms_alone = k1.value / max(1, n1.value)
     achieved_alone = sb0 / (scan_ms_alone * 1e-3) / 1e9
+    xcheck = genome_rows_crosscheck(torch, ctx, gp) if (rank == 0 and args.parity_windows > 0) else None
     # the window statistics alone over the resident rows of the pass (HIP events on the call stream)
     win_ms = None
     if gp.stats:
@@ -617,6 +642,7 @@ def bench_genome(args, torch, dist, world, rank):
             ps = parity_sampled_genome(args, ctx, gp, max(4, args.parity_windows // (2 if args.config == 3 else 1)))
             out["parity_sampled"] = ps["ok"]
             out["parity_sample"] = ps
+            out["rows_crosscheck"] = xcheck
         out["src_sha"] = source_hash()
         print(json.dumps(out), flush=True)
     ctx.close()
