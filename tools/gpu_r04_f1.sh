@@ -1,0 +1,10 @@
+#!/bin/bash
+# r04 final check 1: the whole -m gpu suite + smoke on the round's tree.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; O=gpurun_out/f1; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 \
+    --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log; tail -3 $O/pytest_gpu.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+tail -1 $O/smoke.log
