@@ -35,16 +35,17 @@ CALL_KERNELS = ("call_scan_kernel", "call_slow_kernel", "call_deepq_kernel", "ca
 
 
 def source_hash() -> str:
-    """sha256 over the sources libpopbam_gpu.so is built from (popbam_amd/csrc, include): a PMC
-    profile counts for this build only if it records the same hash."""
+    """sha256 over the sources libpopbam_gpu.so is built from (popbam_amd/csrc minus the host
+    feeder, which is its own library; the headers; include/popbam_gpu.h): a PMC profile counts
+    for this build only if it records the same hash."""
     import glob
     import hashlib
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(REPO, "popbam_amd", "csrc", "*.hip")) +
-                   glob.glob(os.path.join(REPO, "popbam_amd", "csrc", "*.cpp")) +
-                   glob.glob(os.path.join(REPO, "popbam_amd", "csrc", "*.h")) +
-                   [os.path.join(REPO, "popbam_amd", "csrc", "Makefile")] +
-                   glob.glob(os.path.join(REPO, "include", "*.h")))
+    csrc = os.path.join(REPO, "popbam_amd", "csrc")
+    files = sorted([f for f in glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp"))
+                    if os.path.basename(f) != "feeder.cpp"] +
+                   glob.glob(os.path.join(csrc, "*.h")) + [os.path.join(csrc, "Makefile"),
+                                                          os.path.join(REPO, "include", "popbam_gpu.h")])
     for f in files:
         h.update(os.path.relpath(f, REPO).encode() + b"\0")
         with open(f, "rb") as fh:

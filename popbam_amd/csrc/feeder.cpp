@@ -21,6 +21,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <memory>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -107,7 +108,10 @@ struct Inflater {
 // ---------------------------------------------------------------- BGZF
 struct Bgzf {
     FILE *f = nullptr;
-    std::vector<uint8_t> blk;     // uncompressed current block
+    // uncompressed current block: blk[0, blk_n) (BGZF blocks hold at most 64 KiB; the buffer is
+    // never zero-filled, inflate writes every byte)
+    std::unique_ptr<uint8_t[]> blk{new uint8_t[65536]};
+    size_t blk_n = 0;
     size_t at = 0;                // read position in blk
     uint64_t blk_addr = 0;        // file offset of the current block
     uint64_t next_addr = 0;       // file offset of the next block
@@ -126,7 +130,7 @@ struct Bgzf {
         fpos = ~0ull;
         uint8_t h[18];
         size_t got = fread(h, 1, 18, f);
-        blk.clear();
+        blk_n = 0;
         at = 0;
         blk_addr = addr;
         if (got == 0) {
@@ -155,12 +159,13 @@ struct Bgzf {
             return fail(PBF_E_FORMAT, "truncated BGZF block");
         const uint32_t isize = cbuf[cdata + 4] | cbuf[cdata + 5] << 8 | cbuf[cdata + 6] << 16 |
                                (uint32_t)cbuf[cdata + 7] << 24;
-        blk.resize(isize);
+        if (isize > 65536) return fail(PBF_E_FORMAT, "BGZF block larger than 64 KiB");
+        blk_n = isize;
         next_addr = addr + (uint64_t)bsize + 1;
         fpos = next_addr;
         if (isize == 0) return 1;
         const auto t0 = Clock::now();
-        const bool ok = inf.run(cbuf.data(), (size_t)cdata, blk.data(), isize);
+        const bool ok = inf.run(cbuf.data(), (size_t)cdata, blk.get(), isize);
         t_inflate += secs(t0, Clock::now());
         ++n_blocks;
         bytes_in += (uint64_t)cdata;
@@ -179,19 +184,39 @@ struct Bgzf {
         uint8_t *o = (uint8_t *)dst;
         size_t done = 0;
         while (done < n) {
-            if (at >= blk.size()) {
+            if (at >= blk_n) {
                 const int r = load(next_addr);
                 if (r < 0) return r;
                 if (r == 0) break;
                 continue;
             }
-            const size_t k = std::min(n - done, blk.size() - at);
-            memcpy(o + done, blk.data() + at, k);
+            const size_t k = std::min(n - done, blk_n - at);
+            memcpy(o + done, blk.get() + at, k);
             at += k;
             done += k;
         }
         return (long)done;
     }
+    // the next n bytes in place when the current block holds them (the next block is loaded when
+    // the current one is used up); nullptr otherwise (read() then copies across the boundary).
+    // `eof` is set when no byte is left at all.
+    const uint8_t *peek(size_t n, bool &eof, int &err) {
+        eof = false;
+        err = 0;
+        while (at >= blk_n) {
+            const int r = load(next_addr);
+            if (r < 0) {
+                err = r;
+                return nullptr;
+            }
+            if (r == 0) {
+                eof = true;
+                return nullptr;
+            }
+        }
+        return at + n <= blk_n ? blk.get() + at : nullptr;
+    }
+    void skip(size_t n) { at += n; }
 };
 
 // ---------------------------------------------------------------- BAM records
@@ -836,15 +861,32 @@ struct RgIndex {
 // bam_read1 into the arena: 1 = record (kept when of `tid` and overlapping [lo, hi)), 0 = EOF,
 // 2 = past the region (stop), < 0 error
 int read_rec2(Bgzf &z, RecSet &rs, int tid, int32_t lo, int32_t hi, bool has_index, const RgIndex &cf) {
-    uint8_t b4[4];
-    const long g = z.read(b4, 4);
-    if (g == 0) return 0;
-    if (g != 4) return fail(PBF_E_FORMAT, "truncated BAM record");
-    const uint32_t bs = le32(b4);
-    if (bs < 32) return fail(PBF_E_FORMAT, "bad BAM record size");
-    if (rs.scratch.size() < bs) rs.scratch.resize(bs);
-    if (z.read(rs.scratch.data(), bs) != (long)bs) return fail(PBF_E_FORMAT, "truncated BAM record");
-    const uint8_t *p = rs.scratch.data(), *e = p + bs;
+    // the record in place when it lies inside the current block (most do), else copied out
+    bool eof = false;
+    int err = 0;
+    const uint8_t *p = nullptr;
+    uint32_t bs = 0;
+    if (const uint8_t *h = z.peek(4, eof, err)) {
+        bs = le32(h);
+        if (bs >= 32 && (p = z.peek(4 + (size_t)bs, eof, err)) != nullptr) {
+            p += 4;
+            z.skip(4 + (size_t)bs);
+        }
+    }
+    if (err) return err;
+    if (!p) {
+        if (eof) return 0;
+        uint8_t b4[4];
+        const long g = z.read(b4, 4);
+        if (g == 0) return 0;
+        if (g != 4) return fail(PBF_E_FORMAT, "truncated BAM record");
+        bs = le32(b4);
+        if (bs < 32) return fail(PBF_E_FORMAT, "bad BAM record size");
+        if (rs.scratch.size() < bs) rs.scratch.resize(bs);
+        if (z.read(rs.scratch.data(), bs) != (long)bs) return fail(PBF_E_FORMAT, "truncated BAM record");
+        p = rs.scratch.data();
+    }
+    const uint8_t *e = p + bs;
     Rec2 r;
     r.tid = (int32_t)le32(p);
     r.pos = (int32_t)le32(p + 4);
@@ -1106,13 +1148,15 @@ int fast_walk(const RecSet &rs, int32_t cb, int32_t ce, const WalkCfg &cf, const
         for (int s = 0; s < ns; ++s) {
             std::vector<Act> &l = lists[s];
             const size_t na = l.size();
-            Act *A = l.data();
-            size_t w = 0;
+            const Act *A = l.data();
+            bool gone = false;
             uint32_t raw = 0, kk = 0, rq = 0;
             for (size_t j = 0; j < na; ++j) {
-                const Act a = A[j];
-                if (a.end <= pos) continue;   // finished: leaves the buffer
-                A[w++] = a;
+                const Act &a = A[j];
+                if (a.end <= pos) {   // finished: leaves the buffer (compacted below, once)
+                    gone = true;
+                    continue;
+                }
                 const uint16_t c = a.code[pos];
                 if (c == kNoBase || raw >= md) continue;   // no base here; past the sample's max_depth reads
                 ++raw;
@@ -1121,7 +1165,7 @@ int fast_walk(const RecSet &rs, int32_t cb, int32_t ce, const WalkCfg &cf, const
                 kk += c != 0;
                 rq += c ? a.mq2 : 0u;   // rmsq += SQ(core.qual) (popbam.cpp:287)
             }
-            l.resize(w);
+            if (gone) l.erase(std::remove_if(l.begin(), l.end(), [pos](const Act &a) { return a.end <= pos; }), l.end());
             if (kb == 1) {
                 if (kk > 255) return fail(PBF_E_ARG, "more than 255 keys per sample need k_bytes = 2");
                 kout[t0 + s] = (uint8_t)kk;
