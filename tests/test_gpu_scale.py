@@ -150,6 +150,47 @@ def test_rows_only_equals_consensus_word_call(gpu_lib, n, kw, n_sites):
     ctx.close()
 
 
+def _soft_mask(ref: np.ndarray, run: int, every: int) -> np.ndarray:
+    """Lower-case the reference letters of positions [k * every, k * every + run)."""
+    r = ref.copy()
+    pos = np.arange(len(r))
+    letter = np.isin(r & 0x7F, np.frombuffer(b"ACGT", np.uint8))
+    m = ((pos % every) < run) & letter
+    r[m] |= 0x20
+    return r
+
+
+@pytest.mark.parametrize("n,kw", [(12, {}), (24, {"flag": 0x02}), (12, {"min_snpQ": 40}), (20, {"flag": 0x20})])
+def test_soft_masked_reference_runs_match_oracle(gpu_lib, n, kw):
+    """Long lower-case reference runs (soft-masked repeats): POPBAM compares the reference
+    case-sensitively (Appendix A.5), so no key matches it and every called task leaves the
+    scan's reference-only test -- the scan's list fills and the rest go to call_overflow_kernel,
+    which settles uniform / one-error tasks without the sort.  Rows equal the oracle's on both
+    call paths."""
+    import torch
+    from popbam_amd import workload
+    ctx, params = _ctx(n, **kw)
+    n_sites = 64 * max(60, 24000 // n)
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 13 * n)
+    ref = _soft_mask(syn.ref.cpu().numpy(), 3000, 5000)
+    syn.ref.copy_(torch.from_numpy(ref).cuda())
+    hp = workload.HotPath(ctx, syn, [(0, n_sites)], 0)
+    hp.call()
+    ctx.sync_check()
+    rows = hp.rows.cpu().numpy()
+    batch = harness.synth_batch(SEED + 13 * n, 0, n_sites, n, 10, params.max_depth)
+    batch["ref"] = _soft_mask(batch["ref"], 3000, 5000)
+    _, types, _, flags = harness.oracle_call(harness.oracle_params_from(params), batch)
+    expect = harness.rows_from_oracle(types, flags, ctx.row_bytes)
+    bad = np.nonzero(rows != expect)[0] if rows.ndim == 1 else np.nonzero((rows != expect).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} rows differ, first at {bad[0]}"
+    cb = torch.zeros(n_sites * n, dtype=torch.int64, device="cuda")
+    hp.call(cb=cb)
+    ctx.sync_check()
+    assert np.array_equal(hp.rows.cpu().numpy(), expect)
+    ctx.close()
+
+
 def _window_text(ctx, params, hp, cmd_id, output, windows, min_freq=1, jc=0, min_snps=10, flag_sub=False):
     """Format the GPU window outputs with the library's print_<stat> (pbg_format)."""
     from popbam_amd import _lib
