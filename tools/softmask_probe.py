@@ -17,12 +17,13 @@ import torch  # noqa: E402
 from popbam_amd import _lib, workload  # noqa: E402
 
 n_sites = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+fracs = [float(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0.0, 0.1, 0.25, 0.5]
 ctx = _lib.Context(workload.default_params(12), 0)
 syn = workload.SynthPileup(ctx, n_sites, 10, 0xC0FFEE02)
 hp = workload.HotPath(ctx, syn, [(0, n_sites)], 0)
 ref0 = syn.ref.clone()
 out = []
-for frac in (0.0, 0.1, 0.25, 0.5):
+for frac in fracs:
     run = 5000
     pos = torch.arange(n_sites, device="cuda")
     masked = (pos % (run * 100)) < int(frac * run * 100)
