@@ -844,16 +844,45 @@ struct RecSet {
 // the sample of a read group (the callback's partition, popbam.cpp:222-237), looked up without
 // copying the tag (views into the WalkCfg's keys, which outlive the index)
 struct RgIndex {
-    std::unordered_map<std::string_view, int32_t> m;
+    // open addressing over (length, first 8 bytes): one probe and one compare for the few read
+    // groups of a BAM (a std::unordered_map's string hash cost ~1/3 of a record's decode)
+    struct Slot {
+        const char *name = nullptr;
+        uint32_t len = 0;
+        int32_t sample = 0;
+    };
+    std::vector<Slot> t;
+    uint32_t mask = 0;
     int32_t fallback;
     int ns;
+    static uint32_t hash(const char *s, size_t len) {
+        uint64_t w = 0;
+        memcpy(&w, s, std::min<size_t>(len, 8));
+        w ^= (uint64_t)len * 0x9E3779B97F4A7C15ull;
+        w *= 0xBF58476D1CE4E5B9ull;
+        return (uint32_t)(w >> 32);
+    }
     explicit RgIndex(const WalkCfg &cf) : fallback(cf.fallback), ns(cf.ns) {
-        for (const auto &kv : cf.rgmap) m[std::string_view(kv.first)] = kv.second;
+        size_t cap = 16;
+        while (cap < 4 * cf.rgmap.size()) cap *= 2;
+        t.resize(cap);
+        mask = (uint32_t)cap - 1;
+        for (const auto &kv : cf.rgmap) {
+            uint32_t h = hash(kv.first.data(), kv.first.size()) & mask;
+            while (t[h].name && !(t[h].len == kv.first.size() && memcmp(t[h].name, kv.first.data(), t[h].len) == 0))
+                h = (h + 1) & mask;
+            t[h] = Slot{kv.first.data(), (uint32_t)kv.first.size(), kv.second};
+        }
     }
     int32_t sample_of(const char *rg, bool has_rg) const {
         if (!has_rg) return -1;
-        auto it = m.find(std::string_view(rg));
-        const int32_t s = it != m.end() ? it->second : fallback;
+        const size_t len = strlen(rg);
+        int32_t s = fallback;
+        for (uint32_t h = hash(rg, len) & mask; t[h].name; h = (h + 1) & mask)
+            if (t[h].len == len && memcmp(t[h].name, rg, len) == 0) {
+                s = t[h].sample;
+                break;
+            }
         return (s < 0 || s >= ns) ? -2 : s;
     }
 };
