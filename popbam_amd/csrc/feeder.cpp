@@ -1127,6 +1127,8 @@ int fast_walk(const RecSet &rs, int32_t cb, int32_t ce, const WalkCfg &cf, const
     // array over [cb, ce]); a read whose RG has no sample is the fatal error at its first base
     std::vector<std::vector<Act>> lists(ns);
     for (auto &l : lists) l.reserve(64);
+    // per list: the earliest end among its reads (no read leaves before it)
+    std::vector<int32_t> minend((size_t)ns, INT32_MAX);
     std::vector<int32_t> cover((size_t)L + 1, 0);
     int64_t bad_pos = INT64_MAX;
     size_t bad_rec = 0;
@@ -1158,6 +1160,7 @@ int fast_walk(const RecSet &rs, int32_t cb, int32_t ce, const WalkCfg &cf, const
                 continue;
             }
             lists[r.sample].push_back(Act{dst - pos, b, r.sample, (uint32_t)r.mapq * r.mapq, (uint32_t)(idx - 1)});
+            minend[r.sample] = std::min(minend[r.sample], b);
         }
         live += cover[i];
         if (live == 0) {   // no read spans pos: no callback until the next read starts
@@ -1176,25 +1179,36 @@ int fast_walk(const RecSet &rs, int32_t cb, int32_t ce, const WalkCfg &cf, const
         size_t nk = 0;
         for (int s = 0; s < ns; ++s) {
             std::vector<Act> &l = lists[s];
+            if (minend[s] <= pos) {   // some read finished: it leaves the buffer
+                l.erase(std::remove_if(l.begin(), l.end(), [pos](const Act &a) { return a.end <= pos; }), l.end());
+                int32_t me = INT32_MAX;
+                for (const Act &a : l) me = std::min(me, a.end);
+                minend[s] = me;
+            }
             const size_t na = l.size();
             const Act *A = l.data();
-            bool gone = false;
-            uint32_t raw = 0, kk = 0, rq = 0;
-            for (size_t j = 0; j < na; ++j) {
-                const Act &a = A[j];
-                if (a.end <= pos) {   // finished: leaves the buffer (compacted below, once)
-                    gone = true;
-                    continue;
+            uint32_t kk = 0, rq = 0;
+            if (na <= md) {   // max_depth cannot bind: every read with a base here is kept
+                for (size_t j = 0; j < na; ++j) {
+                    const uint16_t c = A[j].code[pos];
+                    const bool key = c != 0 && c != kNoBase;   // a key (0: filtered; no base here)
+                    kd[nk] = c;
+                    nk += key;
+                    kk += key;
+                    rq += key ? A[j].mq2 : 0u;   // rmsq += SQ(core.qual) (popbam.cpp:287)
                 }
-                const uint16_t c = a.code[pos];
-                if (c == kNoBase || raw >= md) continue;   // no base here; past the sample's max_depth reads
-                ++raw;
-                kd[nk] = c;
-                nk += c != 0;
-                kk += c != 0;
-                rq += c ? a.mq2 : 0u;   // rmsq += SQ(core.qual) (popbam.cpp:287)
+            } else {
+                uint32_t raw = 0;
+                for (size_t j = 0; j < na; ++j) {
+                    const uint16_t c = A[j].code[pos];
+                    if (c == kNoBase || raw >= md) continue;   // no base here; past the sample's max_depth reads
+                    ++raw;
+                    kd[nk] = c;
+                    nk += c != 0;
+                    kk += c != 0;
+                    rq += c ? A[j].mq2 : 0u;
+                }
             }
-            if (gone) l.erase(std::remove_if(l.begin(), l.end(), [pos](const Act &a) { return a.end <= pos; }), l.end());
             if (kb == 1) {
                 if (kk > 255) return fail(PBF_E_ARG, "more than 255 keys per sample need k_bytes = 2");
                 kout[t0 + s] = (uint8_t)kk;
