@@ -81,6 +81,23 @@ def _context(params, device: int):
     return ctx
 
 
+_FASTA_CACHE: dict = {}
+
+
+def _reference(path: str, name: str) -> bytes:
+    """The contig's reference sequence, kept across commands in this process like the context
+    (keyed by the FASTA's path, size and modification time, so an edited file is read again)."""
+    from . import feed
+    st = os.stat(path)
+    key = (os.path.realpath(path), st.st_size, st.st_mtime_ns, name)
+    seq = _FASTA_CACHE.get(key)
+    if seq is None:
+        if len(_FASTA_CACHE) >= 4:
+            _FASTA_CACHE.pop(next(iter(_FASTA_CACHE)))
+        seq = _FASTA_CACHE[key] = feed.fasta_fetch(path, name)
+    return seq
+
+
 def _close_contexts():
     while _CTX_CACHE:
         _CTX_CACHE.popitem()[1].close()
@@ -125,7 +142,7 @@ def run(cmd: str, argv: list[str], device: int = 0, rank: int = 0, world: int = 
         tid, beg, end = opt.parse_region(o.region, names, lengths)
         t0 = time.perf_counter()
         try:
-            seq = feed.fasta_fetch(o.reffile, names[tid])
+            seq = _reference(o.reffile, names[tid])
         except feed.FeedError as e:
             raise opt.PopbamError(f"Failed to load index for fastA reference file: {o.reffile}: {e}") from e
         if len(seq) < end:   # positions past the contig's sequence: no reference base
