@@ -261,6 +261,9 @@ struct Batch {
     const uint64_t *block_off;
     const uint16_t *keys;
     int *err;                      // the context's error word (PBG_BOUNDS checks)
+    // the batch has long runs of a lower-case / N reference (the host saw them): the scan then
+    // settles its list mid-block instead of sending what overflows it to call_overflow_kernel
+    int masked;
 };
 
 // PBG_BOUNDS debug build (make bounds -> popbam_amd/variants/bounds/libpopbam_gpu.so): every key

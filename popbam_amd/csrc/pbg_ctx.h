@@ -64,6 +64,7 @@ struct pbg_ctx {
     double *d_lb = nullptr;
     double *d_oe = nullptr;
     int *d_err = nullptr;
+    int scan_masked = 0;   // the next pbg_call_sites' Batch::masked (set by pbg_stream_push from the host reference)
     std::string err;
     // per-pileup LDS staging capacity (keyed by block_off pointer and size), so repeated
     // calls on the same resident batch do not synchronise

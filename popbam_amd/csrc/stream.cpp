@@ -55,6 +55,19 @@ int fail(pbg_ctx *c, int code, const std::string &m) { return pbg::ctx_fail(c, c
 
 int row_bytes_of(const pbg_ctx *c) { return c->row_bytes; }
 
+// The chunk's reference has runs of lower-case / N bases (every 16th position sampled; more
+// than 1 in 64 of them not upper-case A/C/G/T): POPBAM compares the reference case-sensitively
+// (SURVEY Appendix A.5), so every called task there leaves the scan's reference-only test and
+// the scan is told to settle its list mid-block (Batch::masked)
+bool masked_reference(const uint8_t *ref, uint32_t n) {
+    uint32_t odd = 0, seen = 0;
+    for (uint32_t i = 0; i < n; i += 16, ++seen) {
+        const uint8_t b = ref[i] & 0x7F;
+        odd += (b != 'A' && b != 'C' && b != 'G' && b != 'T') ? 1u : 0u;
+    }
+    return seen && odd * 64u > seen;
+}
+
 // pageable caller buffers -> pinned staging: the byte ranges of all jobs split evenly over up
 // to 8 threads (one memcpy stream per thread reaches a fraction of the host's bandwidth)
 struct CopyJob {
@@ -546,7 +559,9 @@ int pbg_stream_push(pbg_stream *st, const pbg_pileup *pc) {
         hipEvent_t c0, c1;
         if ((rc = ev_pair(st, 1, c0, c1))) return st->rc = rc;
         HIPCHK(c, hipEventRecord(c0, b.comp));
+        c->scan_masked = masked_reference(pc->ref + p0, cl) ? 1 : 0;
         rc = pbg_call_sites(c, &dp, (char *)b.d_rows + roff * rb, st->words ? b.d_cb + roff * n : nullptr, b.comp);
+        c->scan_masked = 0;
         if (rc) return st->rc = rc;
         HIPCHK(c, hipEventRecord(c1, b.comp));
         HIPCHK(c, hipEventRecord(s.ev_free, b.comp));

@@ -191,6 +191,48 @@ def test_soft_masked_reference_runs_match_oracle(gpu_lib, n, kw):
     ctx.close()
 
 
+@pytest.mark.parametrize("n,kw", [(12, {}), (24, {"flag": 0x02}), (12, {"min_snpQ": 40})])
+def test_stream_soft_masked_matches_oracle(gpu_lib, n, kw):
+    """The streamed run over a host batch with long lower-case reference runs: pbg_stream_push
+    sees them in the host reference and has the scan settle its list mid-block (Batch::masked)
+    instead of overflowing it; rows equal the oracle's and the resident (overflow-path) call's."""
+    import torch
+    from popbam_amd import _lib, workload
+    import bench
+    ctx, params = _ctx(n, **kw)
+    n_sites = 64 * max(60, 24000 // n)
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 17 * n)
+    ref = _soft_mask(syn.ref.cpu().numpy(), 3000, 5000)
+    syn.ref.copy_(torch.from_numpy(ref).cuda())
+    wins = workload.reference_windows(0, n_sites, 10_000)
+    stats = _lib.PBG_S_NUCDIV | _lib.PBG_S_SFS
+    hp = workload.HotPath(ctx, syn, wins, stats)
+    hp.step()
+    ctx.sync_check()
+
+    class A:
+        window = 10_000
+    cmds, keep = bench.stat_cmds(A, n, 2, 0, n_sites)
+    cmds, keep = cmds[:2], keep   # nucdiv, sfs
+    host = hp.to_host()
+    kb = ctx.k_bytes
+    with _lib.Stream(ctx, cmds, 0, n_sites, 64 * 1000) as st:
+        pl = _lib.PbgPileup(n_sites, 0, host["ref"].data_ptr(), host["k"].data_ptr(), host["rmsq"].data_ptr(),
+                            host["block_off"].data_ptr(), host["keys"].data_ptr())
+        st.push(pl)
+        st.finish()
+        rows = torch.zeros_like(hp.rows)
+        st.rows_into(rows.data_ptr(), rows.numel())
+    assert torch.equal(rows, hp.rows)
+    batch = harness.synth_batch(SEED + 17 * n, 0, n_sites, n, 10, params.max_depth)
+    batch["ref"] = _soft_mask(batch["ref"], 3000, 5000)
+    _, types, _, flags = harness.oracle_call(harness.oracle_params_from(params), batch)
+    expect = harness.rows_from_oracle(types, flags, ctx.row_bytes)
+    got = rows.cpu().numpy()
+    assert np.array_equal(got, expect)
+    ctx.close()
+
+
 def _window_text(ctx, params, hp, cmd_id, output, windows, min_freq=1, jc=0, min_snps=10, flag_sub=False):
     """Format the GPU window outputs with the library's print_<stat> (pbg_format)."""
     from popbam_amd import _lib
