@@ -190,29 +190,71 @@ def cpu_port(args):
                       f"{win} bp windows; excludes BAM decode/pileup"}
 
 
+def host_cpu_share() -> dict:
+    """The host cores this run may use: the machine's count (os.cpu_count / nproc), the scheduler
+    affinity of this process, the cgroup CPU quota, and OMP_NUM_THREADS (the GPU pool's per-box
+    share).  `cores` = the smallest of them: the count every all-core figure below runs with."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    lim = [("affinity", aff)] + ([("cgroup_quota", quota)] if quota else []) + ([("OMP_NUM_THREADS", omp)] if omp else [])
+    by, cores = min(lim, key=lambda x: x[1])
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "omp_num_threads": omp, "cores": cores,
+            "bounded_by": by}
+
+
+_ALL_CORES: dict = {}   # POPBAM region-sharded on every usable core, per (BAM dir): measured once
+
+
+def popbam_all_cores(d: str, L: int, win: int) -> dict:
+    """POPBAM itself (oracle/_ref/popbam) as P concurrent region-sharded processes per command
+    (P = host_cpu_share()['cores'] shards of whole windows), nucdiv + sfs + ld summed; stdout of
+    the shards concatenated = the command's text (the CLI leg compares it with ours)."""
+    import ref_baseline
+    if d not in _ALL_CORES:
+        share = host_cpu_share()
+        t = ref_baseline.time_reference(d, L, win, share["cores"], single=False, capture=True)
+        _ALL_CORES[d] = {"Msites_per_s": round(L / t["parallel_total_s"] / 1e6, 4), "cores": share["cores"],
+                         "processes": t["procs"], "wall_s": round(t["parallel_total_s"], 2),
+                         "per_command_s": {c: round(v, 3) for c, v in t["parallel"].items()},
+                         "host": share, "texts": t["texts"]}
+    return _ALL_CORES[d]
+
+
 def cpu_baseline(args):
     """POPBAM itself (oracle/_ref/popbam, built from /root/reference) on a BAM of the same
     synthetic genome (tests/ref_baseline.py): nucdiv, sfs and ld as three processes, wall times
-    summed, on the first --ref-sample positions; plus P region-sharded processes per command
-    (P = the host's CPU share, at most 16).  The oracle port's rate is reported beside it."""
+    summed, on the first --ref-sample positions (one core); and on every usable host core
+    (host_cpu_share) as region-sharded processes per command over the --cli-sample BAM, which has
+    enough windows for one shard per core.  The oracle port's rate is reported beside it."""
     import ref_baseline
     port = cpu_port(args)
     if args.config == 4 or not ref_baseline.available():   # the reference cannot hold 96 samples
         return port
     L, n = args.ref_sample, args.samples
     d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_v5_{args.seed:x}_{L}_{n}", args.seed, L, n)
-    procs = max(1, min(16, os.cpu_count() or 1))
-    t = ref_baseline.time_reference(d, L, args.window, procs)
+    t = ref_baseline.time_reference(d, L, args.window, 1)
     out = {"value": round(L / t["single_total_s"] / 1e6, 6), "unit": "Msites/s", "cores": 1, "kind": "reference",
            "sample": f"oracle/_ref/popbam (POPBAM 0.3 built from /root/reference) nucdiv, sfs, ld -w "
                      f"{args.window // 1000} as 3 processes (wall {t['single_total_s']:.2f} s summed) on a BAM of "
                      f"positions [0, {L}) of the same synthetic genome: {n} samples, 100 bp reads every 10 bp "
                      f"(depth 10), baseQ 40, mapQ 60, 2 populations; includes BAM decode + pileup",
-           "port": port}
-    if "parallel_total_s" in t:
-        out["all_cores"] = {"value": round(L / t["parallel_total_s"] / 1e6, 6), "cores": t["procs"],
-                            "sample": f"{t['procs']} region-sharded processes per command, concurrent "
-                                      f"(wall {t['parallel_total_s']:.2f} s summed over the 3 commands)"}
+           "host": host_cpu_share(), "port": port}
+    LA = max(args.cli_sample, L)
+    da = ref_baseline.make_inputs(f"/tmp/popbam_refbase_v5_{args.seed:x}_{LA}_{n}", args.seed, LA, n)
+    ac = popbam_all_cores(da, LA, args.window)
+    out["all_cores"] = {"value": ac["Msites_per_s"], "cores": ac["cores"], "processes": ac["processes"],
+                        "sample": f"{ac['processes']} region-sharded processes per command on {ac['cores']} usable "
+                                  f"cores ({ac['host']['bounded_by']}), concurrent, over positions [0, {LA}) "
+                                  f"(wall {ac['wall_s']:.2f} s summed over the 3 commands)"}
     return out
 
 
@@ -329,12 +371,16 @@ def end_to_end(args, torch, ctx, hp, wins) -> dict:
 def cli_rate(args) -> dict:
     """The drop-in command line on a real BAM: `popbam nucdiv|sfs|ld -f ref.fa -w 10 in.bam chr1`
     over a BAM of the first --cli-sample positions of the same synthetic genome
-    (tests/ref_baseline.make_inputs, written natively), each command in-process
-    (popbam_amd.cli.run: feeder workers walk pieces ahead, each piece streamed to the GPU as it
-    comes) with its phase breakdown, and once as a fresh process (interpreter + torch import +
-    context); stdout compared with POPBAM's own on the same BAM, whose region-sharded run on P
-    processes is the all-core rate beside it (3 commands summed, as cpu_baseline)."""
+    (tests/ref_baseline.make_inputs, written natively):
+      - as users run it: a fresh `bin/popbam` process per command (the native host binary,
+        popbam_main.cpp: no interpreter, HIP init + context on a thread beside the feeder's
+        walk), three runs per command, with the binary's own phase profile (POPBAM_PROFILE);
+      - in-process (popbam_amd.cli.run, context and FASTA kept across commands) with its phases;
+      - a fresh Python process (`python -m popbam_amd.cli`, no torch import) for comparison.
+    stdout is compared with POPBAM's own on the same BAM, whose region-sharded run on every usable
+    core is the all-core rate beside it (3 commands summed, as cpu_baseline)."""
     import subprocess
+    import tempfile
 
     import ref_baseline
     from popbam_amd import cli
@@ -343,19 +389,43 @@ def cli_rate(args) -> dict:
     d = ref_baseline.make_inputs(f"/tmp/popbam_refbase_v5_{args.seed:x}_{L}_{n}", args.seed, L, n)
     t_make = time.perf_counter() - t0
     win_kb = str(args.window // 1000)
-    threads = int(os.environ.get("POPBAM_FEED_THREADS", min(16, os.cpu_count() or 1)))
-    os.environ["POPBAM_FEED_THREADS"] = str(threads)
-    res = {"sites": L, "samples": n, "feeder_threads": threads, "bam_bytes": os.path.getsize(os.path.join(d, "in.bam")),
-           "bam_write_s": round(t_make, 2), "commands": {}}
+    share = host_cpu_share()
+    threads = int(os.environ.get("POPBAM_FEED_THREADS", share["cores"]))
+    env = dict(os.environ, POPBAM_FEED_THREADS=str(threads))
+    env.pop("WORLD_SIZE", None)
+    res = {"sites": L, "samples": n, "feeder_threads": threads, "host": share,
+           "bam_bytes": os.path.getsize(os.path.join(d, "in.bam")), "bam_write_s": round(t_make, 2), "commands": {}}
     texts = {}
-    tot_in = tot_proc = 0.0
+    tot_in = tot_proc = tot_py = 0.0
     cwd = os.getcwd()
+    runs = 3
     for c in ("nucdiv", "sfs", "ld"):
         argv = [c, "-f", "ref.fa", "-w", win_kb, "in.bam", "chr1"]
+        # as users run it: a fresh native process per command
+        proc_s, profs, same = [], [], True
+        for _ in range(runs):
+            with tempfile.NamedTemporaryFile(suffix=".json", delete=False) as tf:
+                pf = tf.name
+            t0 = time.perf_counter()
+            p = subprocess.run([os.path.join(REPO, "bin", "popbam"), *argv], cwd=d, capture_output=True,
+                               env=dict(env, POPBAM_PROFILE=pf))
+            proc_s.append(time.perf_counter() - t0)
+            try:
+                with open(pf) as f:
+                    profs.append(json.loads(f.read().splitlines()[-1])["popbam_profile"])
+            except (OSError, ValueError, IndexError):
+                profs.append({})
+            os.unlink(pf)
+            out_native = p.stdout.decode()
+            same = same and p.returncode == 0
+            texts.setdefault(c, out_native)
+            same = same and out_native == texts[c]
+        # in-process (context kept by cli across commands)
+        os.environ["POPBAM_FEED_THREADS"] = str(threads)
         os.chdir(d)
         try:
             best = None
-            for _ in range(2):   # the first run also builds the context (kept by cli for later commands)
+            for _ in range(2):   # the first run also builds the context
                 t0 = time.perf_counter()
                 text = cli.run(c, argv[1:])
                 dt = time.perf_counter() - t0
@@ -363,15 +433,26 @@ def cli_rate(args) -> dict:
                     best = (dt, dict(cli.last_profile))
         finally:
             os.chdir(cwd)
-        texts[c] = text
+        same_in = text == texts[c]
         t0 = time.perf_counter()
-        p = subprocess.run([sys.executable, os.path.join(REPO, "bin", "popbam"), *argv], cwd=d, capture_output=True)
-        t_proc = time.perf_counter() - t0
+        pp = subprocess.run([sys.executable, "-m", "popbam_amd.cli", *argv], cwd=d, capture_output=True,
+                            env=dict(env, PYTHONPATH=REPO))
+        t_py = time.perf_counter() - t0
         pr = best[1]
         fe, gp = pr.get("feeder", {}), pr.get("gpu", {})
+        mean_proc = sum(proc_s) / len(proc_s)
+        keys = ("process_start_to_main_s", "parse_s", "fasta_s", "kstream_open_s", "hip_init_s", "pbg_create_s",
+                "gpu_join_wait_s", "stream_open_s", "walk_push_s", "finish_s", "destroy_s", "run_s", "write_s")
         res["commands"][c] = {
-            "in_process_s": round(best[0], 3), "process_s": round(t_proc, 3),
-            "process_identical": p.returncode == 0 and p.stdout.decode() == text,
+            "process_s": [round(x, 3) for x in proc_s], "process_mean_s": round(mean_proc, 3),
+            "process_identical": same and same_in and pp.returncode == 0 and pp.stdout.decode() == texts[c],
+            "process_phases": {k: round(sum(q.get(k, 0.0) for q in profs) / max(1, len(profs)), 4) for k in keys},
+            "process_phases_note": ("native binary: hip_init_s + pbg_create_s run on a thread while fasta, "
+                                    "kstream_open and the walk's first pieces proceed; gpu_join_wait_s is what the "
+                                    "main thread waited for them; run_s = main's whole run, the rest of process_s "
+                                    "is exec, loading and exit"),
+            "python_process_s": round(t_py, 3),
+            "in_process_s": round(best[0], 3),
             "phases": {"fasta_s": round(pr.get("fasta_s", 0), 3), "context_s": round(pr.get("context_s", 0), 4),
                        "walk_and_push_s": round(pr.get("blocks_s", 0) - gp.get("ms_finish", 0) / 1e3, 3),
                        "feeder_thread_s": {"inflate": round(fe.get("t_inflate", 0), 3),
@@ -385,19 +466,20 @@ def cli_rate(args) -> dict:
                        "h2d_bytes": gp.get("h2d_bytes", 0), "pieces": gp.get("pieces", 0),
                        "inflated_bytes": fe.get("bytes_inflated", 0)}}
         tot_in += best[0]
-        tot_proc += t_proc
-    res["Msites_per_s_in_process"] = round(L / tot_in / 1e6, 4)
+        tot_proc += mean_proc
+        tot_py += t_py
     res["Msites_per_s_process"] = round(L / tot_proc / 1e6, 4)
+    res["Msites_per_s_in_process"] = round(L / tot_in / 1e6, 4)
+    res["Msites_per_s_python_process"] = round(L / tot_py / 1e6, 4)
     if ref_baseline.available():
-        procs = max(1, min(16, os.cpu_count() or 1))
-        t = ref_baseline.time_reference(d, L, args.window, procs, single=False, capture=True)
-        res["popbam_all_cores"] = {"Msites_per_s": round(L / t["parallel_total_s"] / 1e6, 4), "processes": t["procs"],
-                                   "wall_s": round(t["parallel_total_s"], 2)}
-        res["x_over_popbam_all_cores"] = round(res["Msites_per_s_in_process"] / res["popbam_all_cores"]["Msites_per_s"], 2)
-        res["identical_to_reference"] = all(t["texts"][c] == texts[c] for c in texts)
-    res["note"] = ("3 commands summed; in-process = best of 2 runs of popbam_amd.cli.run (feeder threads + GPU, "
-                   "context kept across commands); a fresh process also pays the interpreter, torch import and "
-                   "context creation; feeder_thread_s are summed over worker threads")
+        ac = popbam_all_cores(d, L, args.window)
+        res["popbam_all_cores"] = {k: v for k, v in ac.items() if k != "texts"}
+        res["x_process_over_popbam_all_cores"] = round(res["Msites_per_s_process"] / ac["Msites_per_s"], 2)
+        res["x_in_process_over_popbam_all_cores"] = round(res["Msites_per_s_in_process"] / ac["Msites_per_s"], 2)
+        res["identical_to_reference"] = all(ac["texts"][c] == texts[c] for c in texts)
+    res["note"] = ("3 commands summed; process = mean of 3 fresh `bin/popbam` processes per command (native binary, "
+                   "the drop-in as users run it); in-process = best of 2 runs of popbam_amd.cli.run (context kept "
+                   "across commands); feeder_thread_s are summed over worker threads")
     return res
 
 

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("POPBAM_GPU_LIB") or os.path.join(HERE, "libpopbam_gpu.so")
@@ -91,21 +92,27 @@ class PbgStreamProf(C.Structure):
 _lib = None
 
 
-def load():
+def load(torch_first: bool = True):
+    """Load libpopbam_gpu.so once per process.
+
+    One HIP runtime per process: the PyTorch ROCm wheel bundles its own libamdhip64.so.7 /
+    libhsa-runtime64.so.1 and loads them under different file names.  If this library pulled
+    /opt/rocm's copies in first, torch imported later would load a second HSA runtime that finds
+    no GPU, so processes that use torch (tests, bench.py) import it first (torch_first) and our
+    NEEDED sonames bind to its copies.  The command line never uses torch: it passes
+    torch_first=False and the library runs on the system HIP runtime (no torch import, ~1-2 s of
+    a fresh process), unless torch is already in the process."""
     global _lib
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                            "(there is no CPU fallback)")
-    # One HIP runtime per process: the PyTorch ROCm wheel bundles its own libamdhip64.so.7 /
-    # libhsa-runtime64.so.1 and loads them under different file names.  If this library
-    # pulled /opt/rocm's copies in first, torch would later load a second HSA runtime that
-    # finds no GPU.  Importing torch first makes our NEEDED sonames bind to its copies.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    if torch_first or "torch" in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     lib = C.CDLL(LIB_PATH)
     P = C.POINTER
     vp = C.c_void_p
@@ -168,8 +175,8 @@ class PbgError(RuntimeError):
 class Context:
     """Owns one pbg_ctx (one device)."""
 
-    def __init__(self, params: PbgParams, device: int = 0):
-        self.lib = load()
+    def __init__(self, params: PbgParams, device: int = 0, torch_first: bool = True):
+        self.lib = load(torch_first)
         self.h = C.c_void_p()
         rc = self.lib.pbg_create(C.byref(self.h), device, C.byref(params))
         if rc != PBG_OK:

@@ -77,7 +77,7 @@ def _context(params, device: int):
         if not _CTX_CACHE:
             import atexit
             atexit.register(_close_contexts)
-        ctx = _CTX_CACHE[key] = _lib.Context(params, device)
+        ctx = _CTX_CACHE[key] = _lib.Context(params, device, torch_first=False)
     return ctx
 
 
@@ -136,6 +136,9 @@ def run(cmd: str, argv: list[str], device: int = 0, rank: int = 0, world: int = 
         if not o.reffile or not os.path.exists(o.reffile):
             raise opt.PopbamError(f"Failed to load index for fastA reference file: {o.reffile}")
         sm = opt.parse_header(header, o.bamfile)
+        if o.flag & opt.BAM_OUTGROUP and cmd in ("sfs", "diverge", "snp") and o.outgroup not in sm.samples:
+            # checked right after bam_smpl_add (pop_sfs.cpp:37-50, pop_diverge.cpp:37-50, pop_snp.cpp:36-49)
+            raise opt.PopbamError(f"Specified outgroup {o.outgroup} not found")
         refid = opt.get_refid(header) if cmd == "tree" else ""
         refs = bam.refs
         names, lengths = [r[0] for r in refs], [r[1] for r in refs]
@@ -159,7 +162,10 @@ def run(cmd: str, argv: list[str], device: int = 0, rank: int = 0, world: int = 
             if reg is None:
                 return ""
             (rbeg, rend), ms0 = reg, shard.ms_windows_for(beg, end, o.win_size, windowed, rank)
-        blocks = window_blocks(rbeg, rend, o.win_size, windowed, int(os.environ.get("POPBAM_BLOCK_SITES", 1 << 26)))
+        block_sites = int(os.environ.get("POPBAM_BLOCK_SITES", 1 << 26))
+        if cmd == "snp" and o.output == 0:   # consensus words: n * 8 bytes per position on device and host
+            block_sites = min(block_sites, max(1 << 16, (1 << 30) // (8 * sm.n)))
+        blocks = window_blocks(rbeg, rend, o.win_size, windowed, block_sites)
         if not blocks:   # no window: the reference's loop prints nothing
             return ""
         flt = engine.make_filter(o)

@@ -293,21 +293,31 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         return fail(c, PBG_E_ARG, "keys / k / rmsq / rows must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
     const uint32_t nblk = (pl->n_sites + pbg::kSiteBlock - 1) / pbg::kSiteBlock;
-    if (cb && (c->cap_key != (const void *)pl->block_off || c->cap_sites != pl->n_sites)) {
+    const int64_t hint = c->cap_hint_keys;
+    c->cap_hint_keys = -1;
+    if (cb && (hint >= 0 || c->cap_key != (const void *)pl->block_off || c->cap_sites != pl->n_sites)) {
         // LDS staging capacity of the consensus-word kernel: the mean round plus six standard
         // deviations (Poisson-like), bounded by what one CU can give a workgroup; rounds above
-        // it read HBM directly
+        // it read HBM directly.  The batch's keys are block_off[nblk] - block_off[0] (offsets may
+        // be absolute, include/popbam_gpu.h); a streamed chunk passes its count from the host
         uint64_t total = 0;
-        HIPCHK(c, hipMemcpyAsync(&total, pl->block_off + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost,
-                                 (hipStream_t)stream));
-        HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+        if (hint >= 0) {
+            total = (uint64_t)hint;
+        } else {
+            uint64_t ends[2] = {0, 0};
+            HIPCHK(c, hipMemcpyAsync(&ends[0], pl->block_off, sizeof(uint64_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+            HIPCHK(c, hipMemcpyAsync(&ends[1], pl->block_off + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                     (hipStream_t)stream));
+            HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+            total = ends[1] >= ends[0] ? ends[1] - ends[0] : 0;
+        }
         // keys staged per round = keys of kBlockThreads consecutive (position, sample) tasks
         const double mean = (double)total / ((double)pl->n_sites * c->dp.n) * pbg::kBlockThreads;
         uint32_t cap = (uint32_t)(mean + 6.0 * std::sqrt(mean) + 64.0);
         cap = (cap + 63) & ~63u;
         const uint32_t max_cap = (uint32_t)((48 * 1024 - pbg::call_sites_lds_bytes(c->dp.n, 0)) / 4);
         c->cap_val = std::min(std::max(cap, 256u), max_cap);
-        c->cap_key = pl->block_off;
+        c->cap_key = hint >= 0 ? nullptr : pl->block_off;   // a hinted chunk's slot pointer repeats
         c->cap_sites = pl->n_sites;
     }
     const uint32_t cap = c->cap_val;

@@ -1431,7 +1431,9 @@ int pbf_kstream_next(pbf_kstream *ks, pbf_keys *piece) {
     std::unique_lock<std::mutex> lk(ks->m);
     if (ks->consumed >= ks->nchunk) return 0;
     const auto tw = Clock::now();
-    ks->cv_ready.wait(lk, [&] { return ks->state[ks->consumed] == 1; });
+    // state 2 at `consumed` = a failed piece already reported: the error is sticky (every later
+    // call returns it again instead of waiting for a piece that never comes)
+    ks->cv_ready.wait(lk, [&] { return ks->state[ks->consumed] >= 1; });
     ks->prof.t_consumer_wait += secs(tw, Clock::now());
     const int64_t c = ks->consumed;
     ks->state[c] = 2;

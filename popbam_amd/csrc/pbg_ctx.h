@@ -70,6 +70,8 @@ struct pbg_ctx {
     // calls on the same resident batch do not synchronise
     const void *cap_key = nullptr;
     uint32_t cap_sites = 0, cap_val = 0;
+    int64_t cap_hint_keys = -1;   // the next pbg_call_sites' key count when the caller knows it on the
+                                  // host (pbg_stream_push): no device read, no synchronisation
     // window lists already validated (device pointer, size, rows, statistics), most recent last
     struct Plan {
         const void *wins;

@@ -479,10 +479,12 @@ int pbg_stream_open(pbg_ctx *c, const pbg_cmd *cmds, uint32_t n_cmd, int32_t pos
     return PBG_OK;
 }
 
-int pbg_stream_push(pbg_stream *st, const pbg_pileup *pc) {
-    if (!st || !pc) return PBG_E_ARG;
+}  // extern "C"
+
+namespace {
+
+int stream_push(pbg_stream *st, const pbg_pileup *pc) {
     pbg_ctx *c = st->c;
-    if (st->rc) return st->rc;
     if (st->finished) return fail(c, PBG_E_ARG, "stream already finished");
     if (pc->n_sites == 0) return PBG_OK;
     if (!pc->ref || !pc->k || !pc->rmsq || !pc->keys) return fail(c, PBG_E_ARG, "null pileup array");
@@ -521,7 +523,9 @@ int pbg_stream_push(pbg_stream *st, const pbg_pileup *pc) {
         pbg::StreamSlot &s = b.slot[st->cur];
         st->cur ^= 1;
         const auto tw = Clock::now();
-        int rc = ensure_slot(c, s, st->chunk, nk);
+        // a slot grows to the largest chunk it has held: pieces smaller than the stream's chunk (the
+        // feeder's 64 k-position pieces) pin and allocate only what they need
+        int rc = ensure_slot(c, s, (cl + pbg::kSiteBlock - 1) / pbg::kSiteBlock * pbg::kSiteBlock, nk);
         if (rc) return st->rc = rc;
         if (s.used) HIPCHK(c, hipEventSynchronize(s.ev_in));   // its staging is free again
         st->prof.ms_wait += ms_since(tw);
@@ -560,8 +564,10 @@ int pbg_stream_push(pbg_stream *st, const pbg_pileup *pc) {
         if ((rc = ev_pair(st, 1, c0, c1))) return st->rc = rc;
         HIPCHK(c, hipEventRecord(c0, b.comp));
         c->scan_masked = masked_reference(pc->ref + p0, cl) ? 1 : 0;
+        c->cap_hint_keys = (int64_t)(boff[b1] - boff[b0]);
         rc = pbg_call_sites(c, &dp, (char *)b.d_rows + roff * rb, st->words ? b.d_cb + roff * n : nullptr, b.comp);
         c->scan_masked = 0;
+        c->cap_hint_keys = -1;
         if (rc) return st->rc = rc;
         HIPCHK(c, hipEventRecord(c1, b.comp));
         HIPCHK(c, hipEventRecord(s.ev_free, b.comp));
@@ -573,10 +579,8 @@ int pbg_stream_push(pbg_stream *st, const pbg_pileup *pc) {
     return PBG_OK;
 }
 
-int pbg_stream_finish(pbg_stream *st) {
-    if (!st) return PBG_E_ARG;
+int stream_finish(pbg_stream *st) {
     pbg_ctx *c = st->c;
-    if (st->finished || st->rc) return st->rc;
     const auto t0 = Clock::now();
     st->finished = true;
     if (st->pushed != st->n_sites) return st->rc = fail(c, PBG_E_RANGE, "the pushed pieces do not cover the stream's region");
@@ -598,6 +602,28 @@ int pbg_stream_finish(pbg_stream *st) {
     }
     st->prof.ms_finish = ms_since(t0);
     return PBG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// every failure of push / finish (argument, HIP, batch) is the stream's sticky error: a later
+// push, finish or text of that stream returns it instead of a misleading order / coverage error
+int pbg_stream_push(pbg_stream *st, const pbg_pileup *pc) {
+    if (!st || !pc) return PBG_E_ARG;
+    if (st->rc) return st->rc;
+    const int rc = stream_push(st, pc);
+    if (rc) st->rc = rc;
+    return rc;
+}
+
+int pbg_stream_finish(pbg_stream *st) {
+    if (!st) return PBG_E_ARG;
+    if (st->finished || st->rc) return st->rc;
+    const int rc = stream_finish(st);
+    if (rc) st->rc = rc;
+    return rc;
 }
 
 long pbg_stream_text(pbg_stream *st, uint32_t i, char *out, size_t cap, size_t *needed) {
@@ -637,6 +663,9 @@ void pbg_stream_close(pbg_stream *st) {
         (void)hipSetDevice(st->c->device);
         (void)hipStreamSynchronize(st->c->sb.comp);   // no call may still read a slot / write the rows
         (void)hipStreamSynchronize(st->c->sb.copy);
+        // a stream that failed or never finished may leave kernel flags behind (its pbg_check never
+        // ran): clear them, so the context's next run does not report this one's batch
+        if ((st->rc || !st->finished) && st->c->d_err) (void)hipMemset(st->c->d_err, 0, sizeof(int));
     }
     delete st;
 }

@@ -58,7 +58,7 @@ class _Cmd:
         c.cmd = opt.CMD_IDS[o.cmd]
         c.output, c.min_sites, c.min_snps, c.min_freq = o.output, o.min_sites, o.min_snps, o.min_freq
         c.outidx = 0
-        if o.flag & opt.BAM_OUTGROUP:
+        if o.flag & opt.BAM_OUTGROUP and o.cmd in ("sfs", "diverge", "snp"):   # nucdiv sets the flag, never reads -p
             idx = [i for i, s in enumerate(sm.samples) if s == o.outgroup]
             if not idx:
                 raise opt.PopbamError(f"Specified outgroup {o.outgroup} not found")

@@ -366,3 +366,26 @@ def test_native_synthetic_bam_equals_python_writer(tmp_path):
         outs = [subprocess.run([ref_baseline.REF_BIN, "nucdiv", "-f", "ref.fa", "-w", "5", "in.bam", "chr1:2001-27000"],
                                cwd=d, capture_output=True, check=True).stdout for d in (a, b)]
         assert outs[0] == outs[1] and outs[0].count(b"\n") >= 4
+
+
+def test_kstream_error_is_sticky():
+    """A failing piece (a read group no sample owns: the reference's fatal 'Problem assigning read
+    group', popbam.cpp:234-240) is reported by pbf_kstream_next, and again by every later call
+    instead of a wait for a piece that never comes."""
+    import concurrent.futures as cf
+    c = fixtures.load_case("g01_base")
+    bam = feed.Bam(os.path.join(c["dir"], "in.bam"))
+    seq = feed.fasta_fetch(os.path.join(c["dir"], "ref.fa"), bam.refs[0][0])
+    flt = feed.make_filter(13, 13, 0, 255)
+    ks = bam.key_stream(0, 0, len(seq), seq, {}, 12, 255, flt, -1, threads=2, chunk=4096)
+    with ks:
+        codes = []
+        for _ in range(3):
+            with cf.ThreadPoolExecutor(1) as ex:
+                fut = ex.submit(ks.next)
+                try:
+                    fut.result(timeout=20)
+                    codes.append(0)
+                except feed.FeedError as e:
+                    codes.append(e.code)
+        assert codes == [feed.PBF_E_RG] * 3
