@@ -442,15 +442,16 @@ def cli_rate(args) -> dict:
         fe, gp = pr.get("feeder", {}), pr.get("gpu", {})
         mean_proc = sum(proc_s) / len(proc_s)
         keys = ("process_start_to_main_s", "parse_s", "fasta_s", "kstream_open_s", "hip_init_s", "pbg_create_s",
-                "gpu_join_wait_s", "stream_open_s", "walk_push_s", "finish_s", "destroy_s", "run_s", "write_s")
+                "walk_during_gpu_init_s", "pieces_during_gpu_init", "gpu_join_wait_s", "stream_open_s", "walk_push_s",
+                "finish_s", "run_s", "write_s")
         res["commands"][c] = {
             "process_s": [round(x, 3) for x in proc_s], "process_mean_s": round(mean_proc, 3),
             "process_identical": same and same_in and pp.returncode == 0 and pp.stdout.decode() == texts[c],
             "process_phases": {k: round(sum(q.get(k, 0.0) for q in profs) / max(1, len(profs)), 4) for k in keys},
             "process_phases_note": ("native binary: hip_init_s + pbg_create_s run on a thread while fasta, "
-                                    "kstream_open and the walk's first pieces proceed; gpu_join_wait_s is what the "
-                                    "main thread waited for them; run_s = main's whole run, the rest of process_s "
-                                    "is exec, loading and exit"),
+                                    "kstream_open and the walk proceed (walk_during_gpu_init_s: pieces taken "
+                                    "meanwhile); gpu_join_wait_s is what the main thread then still waited; run_s = "
+                                    "main's whole run, the rest of process_s is exec, library loading and exit"),
             "python_process_s": round(t_py, 3),
             "in_process_s": round(best[0], 3),
             "phases": {"fasta_s": round(pr.get("fasta_s", 0), 3), "context_s": round(pr.get("context_s", 0), 4),

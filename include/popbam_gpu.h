@@ -279,6 +279,9 @@ long pbg_stream_text(pbg_stream *st, uint32_t i, char *out, size_t cap, size_t *
  * memory (the statistics' input: lets a caller check a streamed run against a resident one)   */
 int  pbg_stream_rows(const pbg_stream *st, void *dst, size_t cap);
 int  pbg_stream_profile(const pbg_stream *st, pbg_stream_prof *prof);
+/* the message of the stream's error (its context's last error; "" when it has none): for a
+ * caller that holds the stream but not the context, e.g. a pileup callback                 */
+const char *pbg_stream_error(const pbg_stream *st);
 void pbg_stream_close(pbg_stream *st);
 
 /* ---- profiling ---------------------------------------------------------------------- */

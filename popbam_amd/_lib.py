@@ -29,7 +29,7 @@ EXPORTS = ["pbg_create", "pbg_destroy", "pbg_last_error", "pbg_row_bytes", "pbg_
            "pbg_device_count", "pbg_call_sites", "pbg_window_stats", "pbg_check", "pbg_run", "pbg_take_text",
            "pbg_format", "pbg_set_kernel_timing", "pbg_kernel_time", "pbg_call_time", "pbg_synth_max_keys",
            "pbg_synth_pileup", "pbg_stream_open", "pbg_stream_push", "pbg_stream_finish", "pbg_stream_text",
-           "pbg_stream_rows", "pbg_stream_profile", "pbg_stream_close"]
+           "pbg_stream_rows", "pbg_stream_profile", "pbg_stream_error", "pbg_stream_close"]
 
 
 class PbgParams(C.Structure):
@@ -162,6 +162,8 @@ def load(torch_first: bool = True):
     lib.pbg_stream_rows.restype = C.c_int
     lib.pbg_stream_profile.argtypes = [vp, P(PbgStreamProf)]
     lib.pbg_stream_profile.restype = C.c_int
+    lib.pbg_stream_error.argtypes = [vp]
+    lib.pbg_stream_error.restype = C.c_char_p
     lib.pbg_stream_close.argtypes = [vp]
     lib.pbg_stream_close.restype = None
     _lib = lib

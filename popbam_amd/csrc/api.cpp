@@ -1,6 +1,7 @@
 // api.cpp -- the C-ABI of include/popbam_gpu.h: context, resident-batch launches
 // (pbg_call_sites / pbg_window_stats / pbg_check), the synthetic generator and pbg_format.
 // Streamed runs over host batches (pbg_stream_*, pbg_run) are in stream.cpp.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -66,6 +67,17 @@ hipError_t upload(T **dst, const std::vector<T> &v) {
 }
 
 
+}  // namespace
+
+namespace {
+// errmod_tables.bin beside this library (written by `make`, pbg_host.h)
+std::string tables_path() {
+    Dl_info info;
+    if (!dladdr((void *)&pbg_create, &info) || !info.dli_fname) return std::string();
+    std::string p = info.dli_fname;
+    const size_t sl = p.rfind('/');
+    return (sl == std::string::npos ? std::string(".") : p.substr(0, sl)) + "/errmod_tables.bin";
+}
 }  // namespace
 
 extern "C" {
@@ -160,7 +172,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
         return bad(e, "hipDeviceGetAttribute");
     if (c->n_cu < 1) c->n_cu = 1;
     std::vector<double> fk, beta, lhet;
-    pbg::build_errmod_tables(fk, beta, lhet);
+    if (!pbg::load_errmod_tables(tables_path().c_str(), fk, beta, lhet)) pbg::build_errmod_tables(fk, beta, lhet);
     // the scan's reference-only shortcut needs every beta[q][n][c < n] > 0 (q >= 4, n <= PBG_FAST_MAX)
     for (int q = 4; q < 64; ++q)
         for (int nn = 1; nn <= PBG_FAST_MAX; ++nn)

@@ -6,7 +6,12 @@
 //   LogGamma (integer arguments only)                   gamma.cpp:126-166
 //   calc_a1 / calc_a2 / calc_e1 / calc_e2               pop_sfs.cpp:511-571
 //   r^2 for every (marg1, marg2, c11) of a population    pop_ld.cpp:239-243 (per pop size)
+#include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
 #include <vector>
 
 #include "pbg_host.h"
@@ -55,8 +60,10 @@ void build_errmod_tables(std::vector<double> &fk, std::vector<double> &beta, std
         for (int k = 1; k <= n; ++k) lC[n << 8 | k] = lg[n + 1] - lg[k + 1] - lg[n - k + 1];
 
     // beta[q][n][k] = -10 log10( P(X > k) / P(X >= k) ), X ~ Bin(n, 10^(-q/10)),
-    // summed from the top in long double
-    for (int q = 1; q < 64; ++q) {
+    // summed from the top in long double.  ~2 M expl + logl on the x87 unit (~0.2-0.3 s on one
+    // core, most of a fresh process's context creation): the q planes are independent and each
+    // is computed in the reference's order, so they are split over threads (same bits)
+    auto plane = [&](int q) {
         const double e = std::pow(10.0, -q / 10.0);
         const double le = std::log(e), le1 = std::log(1.0 - e);
         for (int n = 1; n < 256; ++n) {
@@ -68,9 +75,72 @@ void build_errmod_tables(std::vector<double> &fk, std::vector<double> &beta, std
                 above = incl;
             }
         }
-    }
+    };
+    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int q = 1 + t; q < 64; q += nt) plane(q);
+        });
+    for (int q = 1; q < 64; q += nt) plane(q);
+    for (auto &x : th) x.join();
     for (int n = 0; n < 256; ++n)
         for (int k = 0; k < 256; ++k) lhet[n << 8 | k] = lC[n << 8 | k] - ln2 * n;
+}
+
+namespace {
+
+constexpr char kTabMagic[8] = {'P', 'B', 'G', 'T', 'A', 'B', '0', '1'};
+struct TabHeader {
+    char magic[8];
+    uint64_t n_fk, n_beta, n_lhet;
+    uint64_t checksum;   // over the three arrays' bytes, in file order
+};
+
+uint64_t checksum_of(const std::vector<const std::vector<double> *> &parts) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (const auto *v : parts)
+        for (double d : *v) {
+            uint64_t w;
+            std::memcpy(&w, &d, 8);
+            h = (h ^ w) * 0x100000001B3ull;
+            h ^= h >> 29;
+        }
+    return h;
+}
+
+}  // namespace
+
+bool write_errmod_tables(const char *path) {
+    std::vector<double> fk, beta, lhet;
+    build_errmod_tables(fk, beta, lhet);
+    TabHeader h;
+    std::memcpy(h.magic, kTabMagic, 8);
+    h.n_fk = fk.size(), h.n_beta = beta.size(), h.n_lhet = lhet.size();
+    h.checksum = checksum_of({&fk, &beta, &lhet});
+    FILE *f = std::fopen(path, "wb");
+    if (!f) return false;
+    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1;
+    for (const auto *v : {&fk, &beta, &lhet}) ok = ok && std::fwrite(v->data(), 8, v->size(), f) == v->size();
+    return std::fclose(f) == 0 && ok;
+}
+
+bool load_errmod_tables(const char *path, std::vector<double> &fk, std::vector<double> &beta,
+                        std::vector<double> &lhet) {
+    const char *mode = std::getenv("POPBAM_TABLES");
+    if (mode && !std::strcmp(mode, "compute")) return false;
+    FILE *f = path ? std::fopen(path, "rb") : nullptr;
+    if (!f) return false;
+    TabHeader h;
+    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && !std::memcmp(h.magic, kTabMagic, 8) && h.n_fk == 256 &&
+              h.n_beta == 64u * 256u * 256u && h.n_lhet == 256u * 256u;
+    if (ok) {
+        fk.resize(h.n_fk), beta.resize(h.n_beta), lhet.resize(h.n_lhet);
+        for (auto *v : {&fk, &beta, &lhet}) ok = ok && std::fread(v->data(), 8, v->size(), f) == v->size();
+        ok = ok && std::fgetc(f) == EOF && checksum_of({&fk, &beta, &lhet}) == h.checksum;
+    }
+    std::fclose(f);
+    return ok;
 }
 
 void build_sfs_constants(int n, std::vector<double> &a1, std::vector<double> &a2, std::vector<double> &e1,

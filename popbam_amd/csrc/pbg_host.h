@@ -10,6 +10,13 @@
 namespace pbg {
 
 void build_errmod_tables(std::vector<double> &fk, std::vector<double> &beta, std::vector<double> &lhet);
+// The errmod tables are constants (errmod_init(1.0-0.83) has no input): `make` writes them once
+// next to the library (errmod_tables.bin, gen_tables.cpp) and a context reads them back instead
+// of recomputing ~2 M x87 expl/logl (~0.2-0.3 s of every fresh process).  Returns false (and the
+// caller computes them) when the file is absent, of another layout or fails its checksum, or
+// when POPBAM_TABLES=compute.
+bool write_errmod_tables(const char *path);
+bool load_errmod_tables(const char *path, std::vector<double> &fk, std::vector<double> &beta, std::vector<double> &lhet);
 void build_sfs_constants(int n, std::vector<double> &a1, std::vector<double> &a2, std::vector<double> &e1,
                          std::vector<double> &e2);
 void build_r2_table(int n_pop, std::vector<double> &t);

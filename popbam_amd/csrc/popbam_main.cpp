@@ -35,6 +35,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -526,6 +527,7 @@ int env_int(const char *name, long dflt) {
 // ---- the GPU context, built on its own thread -------------------------------------------
 struct GpuInit {
     std::thread th;
+    std::atomic<bool> done{false};
     pbg_params P{};
     int device = 0, rc = PBG_OK;
     pbg_ctx *ctx = nullptr;
@@ -543,6 +545,7 @@ struct GpuInit {
             if (rc != PBG_OK) err = pbg_last_error(nullptr);
             t_hip_init = secs(t0, t1);
             t_create = secs(t1, Clock::now());
+            done.store(true);
         });
     }
     void join() {
@@ -695,7 +698,38 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
             ~KsCloser() { pbf_kstream_close(k); }
         } ks_closer{ks};
         prof.add("kstream_open_s", secs(t0, Clock::now()));
-        if (!ctx) {   // the context thread: HIP init + tables overlapped with the walk's start
+        // Until the context thread is done (HIP init + tables), take the walk's pieces as they come
+        // (up to ~1 GB), so the feeder's workers never stall on their look-ahead: the walk of a
+        // fresh process's first block overlaps the GPU's initialisation instead of following it
+        std::vector<pbf_keys> early;
+        bool walked = false;
+        struct EarlyFree {
+            std::vector<pbf_keys> &v;
+            ~EarlyFree() {
+                for (auto &p : v) pbf_keys_free(&p);
+            }
+        } early_free{early};
+        if (!ctx) {
+            t0 = Clock::now();
+            size_t held = 0;
+            while (!gi.done.load() && held < (1u << 30)) {
+                pbf_keys p{};
+                const int r = pbf_kstream_next(ks, &p);
+                if (r < 0) {
+                    if (r == PBF_E_RG) throw Fatal{"Problem assigning read group"};
+                    throw Fatal{"Failed to retrieve region " + o.region + ": " + pbf_last_error()};
+                }
+                if (r == 0) {
+                    walked = true;
+                    break;
+                }
+                held += (size_t)p.n_sites * (1 + (size_t)n * (flt.k_bytes + 4)) + p.n_keys * 2;
+                early.push_back(p);
+            }
+            prof.add("walk_during_gpu_init_s", secs(t0, Clock::now()));
+            prof.add("pieces_during_gpu_init", (double)early.size());
+        }
+        if (!ctx) {   // the context thread: HIP init + tables
             t0 = Clock::now();
             gi.join();
             prof.add("gpu_join_wait_s", secs(t0, Clock::now()));
@@ -714,14 +748,24 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
         } st_closer{st};
         prof.add("stream_open_s", secs(t0, Clock::now()));
         t0 = Clock::now();
-        for (;;) {
+        for (pbf_keys &p : early) {
+            pbg_pileup pl{p.n_sites, p.pos0, p.ref, p.k, p.rmsq, p.block_off, p.keys};
+            const int pr = pbg_stream_push(st, &pl);
+            pbf_keys_free(&p);
+            if (pr != PBG_OK) throw Fatal{std::string("pbg_stream_push failed: ") + pbg_last_error(ctx)};
+        }
+        early.clear();
+        while (!walked) {
             pbf_keys p{};
             const int r = pbf_kstream_next(ks, &p);
             if (r < 0) {
                 if (r == PBF_E_RG) throw Fatal{"Problem assigning read group"};
                 throw Fatal{"Failed to retrieve region " + o.region + ": " + pbf_last_error()};
             }
-            if (r == 0) break;
+            if (r == 0) {
+                walked = true;
+                break;
+            }
             pbg_pileup pl{p.n_sites, p.pos0, p.ref, p.k, p.rmsq, p.block_off, p.keys};
             const int pr = pbg_stream_push(st, &pl);
             pbf_keys_free(&p);
@@ -752,10 +796,12 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
         }
         ++prof.blocks;
     }
-    t0 = Clock::now();
-    if (ctx) pbg_destroy(ctx);
-    prof.add("destroy_s", secs(t0, Clock::now()));
     prof.add("run_s", secs(t_start, Clock::now()));
+    // the process ends right after this run (main exits with _exit): every stream has finished and
+    // been closed, so nothing is in flight, and the context's device memory goes with the process
+    // (pbg_destroy and the HIP runtime's teardown cost a fresh process ~0.15 s).  POPBAM_DESTROY=1
+    // destroys it here all the same.
+    if (ctx && env_int("POPBAM_DESTROY", 0)) pbg_destroy(ctx);
     return text;
 }
 
@@ -900,11 +946,13 @@ int main(int argc, char **argv) {
     } catch (const Fatal &f) {
         fatal_text(f.msg);
         emit_profile(prof);
-        return 1;
+        std::fflush(nullptr);
+        _exit(1);
     }
     const auto t0 = Clock::now();
     const bool ok = write_all(1, text.data(), text.size());
     prof.add("write_s", secs(t0, Clock::now()));
     emit_profile(prof);
-    return ok ? 0 : 1;
+    std::fflush(nullptr);
+    _exit(ok ? 0 : 1);   // see run(): no teardown of the device context / HIP runtime at exit
 }

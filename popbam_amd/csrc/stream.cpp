@@ -657,6 +657,12 @@ int pbg_stream_profile(const pbg_stream *st, pbg_stream_prof *p) {
     return PBG_OK;
 }
 
+const char *pbg_stream_error(const pbg_stream *st) {
+    if (!st) return "null stream";
+    if (!st->rc) return "";
+    return pbg_last_error(st->c);
+}
+
 void pbg_stream_close(pbg_stream *st) {
     if (!st) return;
     if (st->c && st->c->sb.comp) {

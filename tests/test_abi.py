@@ -53,3 +53,24 @@ def test_feeder_exports_header_symbols():
     lib = feed.load()
     for nm in names:
         assert hasattr(lib, nm), nm
+
+
+def test_errmod_table_file_equals_the_oracles_cal_coef():
+    """popbam_amd/errmod_tables.bin (written by `make`, read by every pbg_create instead of
+    recomputing ~2 M x87 expl/logl) holds exactly the oracle's cal_coef tables
+    (pop_utils.cpp:203-266): fk, beta, lhet, bit for bit, after a 48-byte header."""
+    import numpy as np
+
+    import harness
+    path = os.path.join(REPO, "popbam_amd", "errmod_tables.bin")
+    raw = np.fromfile(path, dtype=np.uint8)
+    assert raw[:8].tobytes() == b"PBGTAB01"
+    n_fk, n_beta, n_lhet = np.frombuffer(raw[8:32].tobytes(), np.uint64)
+    body = np.frombuffer(raw[40:].tobytes(), np.float64)
+    assert (n_fk, n_beta, n_lhet) == (256, 64 * 256 * 256, 256 * 256) and body.size == n_fk + n_beta + n_lhet
+    lib = harness.oracle()
+    for nm, off, cnt in (("orc_fk", 0, n_fk), ("orc_beta", n_fk, n_beta), ("orc_lhet", n_fk + n_beta, n_lhet)):
+        f = getattr(lib, nm)
+        f.restype = C.POINTER(C.c_double)
+        want = np.ctypeslib.as_array(f(), (int(cnt),))
+        assert np.array_equal(body[off:off + cnt].view(np.uint64), want.view(np.uint64)), nm
