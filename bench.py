@@ -406,13 +406,20 @@ def cli_rate(args) -> dict:
         for _ in range(runs):
             with tempfile.NamedTemporaryFile(suffix=".json", delete=False) as tf:
                 pf = tf.name
-            t0 = time.perf_counter()
+            t0, w0 = time.perf_counter(), time.time()
             p = subprocess.run([os.path.join(REPO, "bin", "popbam"), *argv], cwd=d, capture_output=True,
                                env=dict(env, POPBAM_PROFILE=pf))
             proc_s.append(time.perf_counter() - t0)
+            w1 = time.time()
             try:
                 with open(pf) as f:
-                    profs.append(json.loads(f.read().splitlines()[-1])["popbam_profile"])
+                    q = json.loads(f.read().splitlines()[-1])["popbam_profile"]
+                # wall clock: spawn -> main, and _exit -> reaped by this process (kernel teardown)
+                q["spawn_to_main_s"] = q.pop("main_wall_epoch_s", w0) - w0
+                q["exit_to_reaped_s"] = w1 - q.pop("exit_wall_epoch_s", w1)
+                for k2 in ("ms_stage", "ms_wait", "ms_h2d", "ms_call"):
+                    q["gpu_" + k2] = q.get("gpu", {}).get(k2, 0.0)
+                profs.append(q)
             except (OSError, ValueError, IndexError):
                 profs.append({})
             os.unlink(pf)
@@ -441,9 +448,10 @@ def cli_rate(args) -> dict:
         pr = best[1]
         fe, gp = pr.get("feeder", {}), pr.get("gpu", {})
         mean_proc = sum(proc_s) / len(proc_s)
-        keys = ("process_start_to_main_s", "parse_s", "fasta_s", "kstream_open_s", "hip_init_s", "pbg_create_s",
-                "walk_during_gpu_init_s", "pieces_during_gpu_init", "gpu_join_wait_s", "stream_open_s", "walk_push_s",
-                "finish_s", "run_s", "write_s")
+        keys = ("spawn_to_main_s", "parse_s", "fasta_s", "kstream_open_s", "hip_init_s", "pbg_create_s",
+                "walk_during_gpu_init_s", "pieces_during_gpu_init", "gpu_join_wait_s", "stream_open_s", "first_push_s",
+                "push_early_s", "walk_push_s", "gpu_ms_stage", "gpu_ms_wait", "gpu_ms_h2d", "gpu_ms_call", "finish_s",
+                "run_s", "write_s", "exit_to_reaped_s")
         res["commands"][c] = {
             "process_s": [round(x, 3) for x in proc_s], "process_mean_s": round(mean_proc, 3),
             "process_identical": same and same_in and pp.returncode == 0 and pp.stdout.decode() == texts[c],

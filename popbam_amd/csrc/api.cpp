@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -381,7 +382,11 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         ++c->ev_used;
         HIPCHK(c, hipEventRecord(c0, (hipStream_t)stream));
     }
-    const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys, c->d_err, c->scan_masked};
+    uint32_t shrink = 0;
+#ifdef PBG_BOUNDS
+    if (const char *st = std::getenv("PBG_BOUNDS_SELFTEST")) shrink = std::atoi(st) > 0 ? 8u : 0u;
+#endif
+    const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys, c->d_err, c->scan_masked, shrink};
     HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, B, cap, rows, cb, c->d_err, c->deep,
                                      (hipStream_t)stream, e0, e1, c->n_cu));
     if (c1) HIPCHK(c, hipEventRecord(c1, (hipStream_t)stream));

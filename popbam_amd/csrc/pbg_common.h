@@ -264,6 +264,10 @@ struct Batch {
     // the batch has long runs of a lower-case / N reference (the host saw them): the scan then
     // settles its list mid-block instead of sending what overflows it to call_overflow_kernel
     int masked;
+    // PBG_BOUNDS builds only: keys the checks take off the end of the batch's range (the
+    // positive control, PBG_BOUNDS_SELFTEST=1: the batch's last chunk counts as outside, so a
+    // correct kernel trips the check and pbg_check must report it); 0 otherwise
+    uint32_t bounds_shrink;
 };
 
 // PBG_BOUNDS debug build (make bounds -> popbam_amd/variants/bounds/libpopbam_gpu.so): every key
@@ -275,11 +279,11 @@ struct Batch {
 __device__ __forceinline__ void bounds_range(const Batch &B, uint64_t lo, uint64_t n) {   // key indices [lo, lo + n)
     if (n == 0) return;
     const uint32_t nblk = (B.n_sites + kSiteBlock - 1) / kSiteBlock;
-    if (lo < B.block_off[0] || lo + n > B.block_off[nblk]) atomicOr(B.err, 8);
+    if (lo < B.block_off[0] || lo + n + B.bounds_shrink > B.block_off[nblk]) atomicOr(B.err, 8);
 }
 __device__ __forceinline__ void bounds_chunk(const Batch &B, uint64_t c) {   // 16-byte chunk c of keys[]
     const uint32_t nblk = (B.n_sites + kSiteBlock - 1) / kSiteBlock;
-    if (8 * c + 8 <= B.block_off[0] || 8 * c >= B.block_off[nblk]) atomicOr(B.err, 8);
+    if (8 * c + 8 <= B.block_off[0] || 8 * c + B.bounds_shrink >= B.block_off[nblk]) atomicOr(B.err, 8);
 }
 #define PBG_BOUNDS_KEYS(B, lo, n) ::pbg::bounds_range((B), (lo), (n))
 #define PBG_BOUNDS_CHUNK(B, c) ::pbg::bounds_chunk((B), (c))

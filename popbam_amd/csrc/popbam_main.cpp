@@ -699,7 +699,7 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
         } ks_closer{ks};
         prof.add("kstream_open_s", secs(t0, Clock::now()));
         // Until the context thread is done (HIP init + tables), take the walk's pieces as they come
-        // (up to ~1 GB), so the feeder's workers never stall on their look-ahead: the walk of a
+        // (up to ~3 GB), so the feeder's workers never stall on their look-ahead: the walk of a
         // fresh process's first block overlaps the GPU's initialisation instead of following it
         std::vector<pbf_keys> early;
         bool walked = false;
@@ -712,7 +712,7 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
         if (!ctx) {
             t0 = Clock::now();
             size_t held = 0;
-            while (!gi.done.load() && held < (1u << 30)) {
+            while (!gi.done.load() && held < (3ull << 30)) {
                 pbf_keys p{};
                 const int r = pbf_kstream_next(ks, &p);
                 if (r < 0) {
@@ -748,12 +748,17 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
         } st_closer{st};
         prof.add("stream_open_s", secs(t0, Clock::now()));
         t0 = Clock::now();
+        bool first = true;
         for (pbf_keys &p : early) {
+            const auto tp = Clock::now();
             pbg_pileup pl{p.n_sites, p.pos0, p.ref, p.k, p.rmsq, p.block_off, p.keys};
             const int pr = pbg_stream_push(st, &pl);
             pbf_keys_free(&p);
             if (pr != PBG_OK) throw Fatal{std::string("pbg_stream_push failed: ") + pbg_last_error(ctx)};
+            if (first) prof.add("first_push_s", secs(tp, Clock::now()));
+            first = false;
         }
+        prof.add("push_early_s", secs(t0, Clock::now()));
         early.clear();
         while (!walked) {
             pbf_keys p{};
@@ -940,6 +945,7 @@ int main(int argc, char **argv) {
     }
     Profile prof;
     prof.add("process_start_to_main_s", since_process_start());
+    prof.add("main_wall_epoch_s", std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count());
     std::string text;
     try {
         text = run(cmd, args, env_int("POPBAM_DEVICE", 0), 0, 1, prof);
@@ -952,6 +958,7 @@ int main(int argc, char **argv) {
     const auto t0 = Clock::now();
     const bool ok = write_all(1, text.data(), text.size());
     prof.add("write_s", secs(t0, Clock::now()));
+    prof.add("exit_wall_epoch_s", std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count());
     emit_profile(prof);
     std::fflush(nullptr);
     _exit(ok ? 0 : 1);   // see run(): no teardown of the device context / HIP runtime at exit
