@@ -196,6 +196,11 @@ int pbg_window_stats(pbg_ctx *ctx, const void *rows, uint32_t n_rows, const pbg_
  * ran out -- the windows that could not get a slice have unset outputs. */
 int pbg_check(pbg_ctx *ctx, void *stream);
 
+/* "product" for the shipped build; "bounds" for the PBG_BOUNDS debug build (key loads checked);
+ * "experiment" for a timing variant built with experiment switches (tools/variant.sh) -- some of
+ * which give wrong results, so nothing may ship or benchmark one as the product. */
+const char *pbg_build_info(void);
+
 /* ---- one subcommand end to end ------------------------------------------------------ */
 enum { PBG_CMD_SNP = 0, PBG_CMD_HAPLO = 1, PBG_CMD_DIVERGE = 2, PBG_CMD_TREE = 3,
        PBG_CMD_NUCDIV = 4, PBG_CMD_LD = 5, PBG_CMD_SFS = 6 };   /* popbam_func_t (popbam.h:208) */

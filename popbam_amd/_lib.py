@@ -27,7 +27,7 @@ PBG_S_TREE = 0x400
 # every symbol include/popbam_gpu.h declares
 EXPORTS = ["pbg_create", "pbg_destroy", "pbg_last_error", "pbg_row_bytes", "pbg_k_bytes", "pbg_sfs_stride",
            "pbg_device_count", "pbg_call_sites", "pbg_window_stats", "pbg_check", "pbg_run", "pbg_take_text",
-           "pbg_format", "pbg_set_kernel_timing", "pbg_kernel_time", "pbg_call_time", "pbg_synth_max_keys",
+           "pbg_format", "pbg_build_info", "pbg_set_kernel_timing", "pbg_kernel_time", "pbg_call_time", "pbg_synth_max_keys",
            "pbg_synth_pileup", "pbg_stream_open", "pbg_stream_push", "pbg_stream_finish", "pbg_stream_text",
            "pbg_stream_rows", "pbg_stream_profile", "pbg_stream_error", "pbg_stream_close"]
 
@@ -131,6 +131,8 @@ def load(torch_first: bool = True):
     lib.pbg_call_sites.restype = C.c_int
     lib.pbg_window_stats.argtypes = [vp, vp, C.c_uint32, vp, C.c_uint32, P(PbgStatOpts), P(PbgWindowOut), vp]
     lib.pbg_window_stats.restype = C.c_int
+    lib.pbg_build_info.argtypes = []
+    lib.pbg_build_info.restype = C.c_char_p
     lib.pbg_check.argtypes = [vp, vp]
     lib.pbg_check.restype = C.c_int
     lib.pbg_take_text.argtypes = [vp, C.c_char_p, C.c_size_t]

@@ -70,6 +70,10 @@ hipError_t upload(T **dst, const std::vector<T> &v) {
 
 }  // namespace
 
+namespace pbg {
+extern const int kBuildKind_call, kBuildKind_stats;
+}
+
 namespace {
 // errmod_tables.bin beside this library (written by `make`, pbg_host.h)
 std::string tables_path() {
@@ -391,6 +395,11 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
                                      (hipStream_t)stream, e0, e1, c->n_cu));
     if (c1) HIPCHK(c, hipEventRecord(c1, (hipStream_t)stream));
     return PBG_OK;
+}
+
+const char *pbg_build_info(void) {
+    const int kind = std::max({(int)PBG_BUILD_KIND, pbg::kBuildKind_call, pbg::kBuildKind_stats});
+    return kind == 2 ? "experiment" : kind == 1 ? "bounds" : "product";
 }
 
 int pbg_check(pbg_ctx *c, void *stream) {

@@ -7,6 +7,26 @@
 #define PBG_HD __host__ __device__
 #include "pbg_key.h"
 
+// Experiment switches (timing variants; PBG_SLOW_NONET and PBG_ZNS_EXP even give wrong results)
+// compile only in a variant build that says so: tools/variant.sh adds -DPBG_EXPERIMENT=1.  The
+// product build (popbam_csrc/Makefile) cannot take one by accident, and every translation unit
+// records its build kind for pbg_build_info() (product / bounds / experiment).
+#if !defined(PBG_EXPERIMENT)
+#if defined(PBG_SLOW_NONET) || defined(PBG_ZNS_EXP) || defined(PBG_ZNS_SORT) || defined(PBG_ZNS_PRIO) || \
+    defined(PBG_SCAN_WIDE_PASS) || defined(PBG_CALL_WAVES_PER_SIMD) || defined(PBG_SLOW_WG_PER_CU) ||      \
+    defined(PBG_WIN_AHEAD) || defined(PBG_FAST_MAX)
+#error "an experiment switch is defined: build variants with tools/variant.sh (-DPBG_EXPERIMENT=1)"
+#endif
+#define PBG_BUILD_KIND (PBG_BOUNDS_KIND)
+#else
+#define PBG_BUILD_KIND 2
+#endif
+#ifdef PBG_BOUNDS
+#define PBG_BOUNDS_KIND 1
+#else
+#define PBG_BOUNDS_KIND 0
+#endif
+
 namespace pbg {
 
 constexpr int kBlockThreads = 256;     // 4 wave64 per workgroup

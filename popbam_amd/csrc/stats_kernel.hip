@@ -23,6 +23,10 @@
 #include "pbg_common.h"
 
 namespace pbg {
+extern const int kBuildKind_stats = PBG_BUILD_KIND;   // pbg_build_info()
+}
+
+namespace pbg {
 
 namespace {
 

@@ -74,3 +74,18 @@ def test_errmod_table_file_equals_the_oracles_cal_coef():
         f.restype = C.POINTER(C.c_double)
         want = np.ctypeslib.as_array(f(), (int(cnt),))
         assert np.array_equal(body[off:off + cnt].view(np.uint64), want.view(np.uint64)), nm
+
+
+def test_build_kinds():
+    """The shipped library reports "product"; the PBG_BOUNDS build "bounds"; experiment switches
+    (some give wrong results) cannot compile into a product build (pbg_common.h #error)."""
+    assert _lib.load().pbg_build_info() == b"product"
+    b = os.path.join(REPO, "popbam_amd", "variants", "bounds", "libpopbam_gpu.so")
+    if os.path.exists(b):
+        lib = C.CDLL(b)
+        lib.pbg_build_info.restype = C.c_char_p
+        assert lib.pbg_build_info() == b"bounds"
+    import subprocess
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-fsyntax-only", "-x", "hip", "--offload-arch=gfx950", "-DPBG_SLOW_NONET",
+                        os.path.join(REPO, "popbam_amd", "csrc", "call_kernel.hip")], capture_output=True, text=True)
+    assert r.returncode != 0 and "experiment switch" in r.stderr, r.stderr[-500:]
