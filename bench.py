@@ -450,7 +450,7 @@ def cli_rate(args) -> dict:
         mean_proc = sum(proc_s) / len(proc_s)
         keys = ("spawn_to_main_s", "parse_s", "fasta_s", "kstream_open_s", "hip_init_s", "pbg_create_s",
                 "walk_during_gpu_init_s", "pieces_during_gpu_init", "gpu_join_wait_s", "stream_open_s", "first_push_s",
-                "push_early_s", "walk_push_s", "gpu_ms_stage", "gpu_ms_wait", "gpu_ms_h2d", "gpu_ms_call", "finish_s",
+                "push_early_s", "push_calls_s", "keys_free_s", "walk_push_s", "gpu_ms_stage", "gpu_ms_wait", "gpu_ms_h2d", "gpu_ms_call", "finish_s",
                 "run_s", "write_s", "exit_to_reaped_s")
         res["commands"][c] = {
             "process_s": [round(x, 3) for x in proc_s], "process_mean_s": round(mean_proc, 3),

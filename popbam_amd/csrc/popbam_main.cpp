@@ -753,7 +753,10 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
             const auto tp = Clock::now();
             pbg_pileup pl{p.n_sites, p.pos0, p.ref, p.k, p.rmsq, p.block_off, p.keys};
             const int pr = pbg_stream_push(st, &pl);
+            const auto tf = Clock::now();
             pbf_keys_free(&p);
+            prof.add("push_calls_s", secs(tp, tf));
+            prof.add("keys_free_s", secs(tf, Clock::now()));
             if (pr != PBG_OK) throw Fatal{std::string("pbg_stream_push failed: ") + pbg_last_error(ctx)};
             if (first) prof.add("first_push_s", secs(tp, Clock::now()));
             first = false;

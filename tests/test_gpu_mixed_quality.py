@@ -7,7 +7,7 @@ slow paths' float rms were pinned only by a small golden fixture.  Here the gene
 are rewritten on the host: baseQ uniform in 2..41, and per position a fraction f ~ U(0, 0.7) of
 reads takes a mapQ from {0, 10, 13, 20, 29, 37, 45} (the rest 60), over three depth regimes
 (mean depth 2, 8 and 15: per-sample depths ~0..30).  With min_rmsQ 25 and 45 samples pass and
-fail on rms around the threshold (about 30-40 % of (position, sample) cells fail).
+fail on rms around the threshold (at 25, ~9 % of (position, sample) cells fail it alone).
 
 Each batch goes to the GPU three ways and must equal the CPU oracle (orc_call_sites, the
 reference's call chain restated) bit for bit:
@@ -147,4 +147,4 @@ def test_mixed_quality_calls_match_oracle(gpu_lib, n, chunk, total, min_rmsq):
     finally:
         ctx.close()
     # the rms test binds: many cells fail it, yet many positions are counted
-    assert counted > total // 50 and failed > total * n // 10, (counted, failed)
+    assert counted > total // 50 and failed > total * n // 25, (counted, failed)
