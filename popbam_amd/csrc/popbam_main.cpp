@@ -37,12 +37,14 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -524,6 +526,52 @@ int env_int(const char *name, long dflt) {
     return v && *v ? (int)std::strtol(v, nullptr, 10) : (int)dflt;
 }
 
+// ---- pieces are freed on a thread of their own ---------------------------------------------
+// A piece's arrays are tens of MB (munmap + TLB shootdowns across the feeder's threads: ~1.4 ms
+// each, ~0.1 s per 5 Mbp command on the main thread); the process ends right after its run, so
+// whatever is still queued then goes with it.
+struct Freer {
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<pbf_keys> q;
+    bool stop = false;
+    std::thread th;
+    Freer() {
+        th = std::thread([this] {
+            std::unique_lock<std::mutex> lk(m);
+            for (;;) {
+                cv.wait(lk, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;
+                std::vector<pbf_keys> batch;
+                batch.swap(q);
+                lk.unlock();
+                for (auto &p : batch) pbf_keys_free(&p);
+                lk.lock();
+            }
+        });
+    }
+    void put(const pbf_keys &p) {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            q.push_back(p);
+        }
+        cv.notify_one();
+    }
+    ~Freer() {   // normal teardown (errors, POPBAM_DESTROY): drain and join
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_one();
+        th.join();
+    }
+};
+
+Freer *freer() {   // one per process, never destroyed (see above)
+    static Freer *f = new Freer();
+    return f;
+}
+
 // ---- the GPU context, built on its own thread -------------------------------------------
 struct GpuInit {
     std::thread th;
@@ -754,7 +802,7 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
             pbg_pileup pl{p.n_sites, p.pos0, p.ref, p.k, p.rmsq, p.block_off, p.keys};
             const int pr = pbg_stream_push(st, &pl);
             const auto tf = Clock::now();
-            pbf_keys_free(&p);
+            freer()->put(p);
             prof.add("push_calls_s", secs(tp, tf));
             prof.add("keys_free_s", secs(tf, Clock::now()));
             if (pr != PBG_OK) throw Fatal{std::string("pbg_stream_push failed: ") + pbg_last_error(ctx)};
@@ -776,7 +824,7 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
             }
             pbg_pileup pl{p.n_sites, p.pos0, p.ref, p.k, p.rmsq, p.block_off, p.keys};
             const int pr = pbg_stream_push(st, &pl);
-            pbf_keys_free(&p);
+            freer()->put(p);
             if (pr != PBG_OK) throw Fatal{std::string("pbg_stream_push failed: ") + pbg_last_error(ctx)};
         }
         prof.add("walk_push_s", secs(t0, Clock::now()));
