@@ -1209,10 +1209,12 @@ extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int3
         depth[s] = (uint16_t)d;
         int a0 = (snp && (uint32_t)(hs & 0xFFFF) < f16) ? alt : ref_idx;
         int a1 = (snp && (uint32_t)((hs >> 16) & 0xFFFF) < f16) ? alt : ref_idx;
-        // reads = template entries [o, o + d) (pbg_common.h synth_tmpl_*)
-        const uint32_t o = (uint32_t)((hs >> 32) & ((1u << 17) - 1)) * 8u;
+        // read r = template entry base + 8 (s + n (r >> 3)) + (r & 7), base a multiple of 64 from
+        // bits 32..45 of the site hash (pbg_common.h synth_tmpl_base / synth_tmpl_index / _entry)
+        const uint32_t base = (uint32_t)((h >> 32) & ((1u << 14) - 1)) * 64u;
         for (int r = 0; r < d; ++r) {
-            uint32_t hr = tseed ^ (0x9E3779B9u * (o + (uint32_t)r + 1u));   // mix32 (lowbias32)
+            const uint32_t idx = base + 8u * ((uint32_t)s + (uint32_t)n * ((uint32_t)r >> 3)) + ((uint32_t)r & 7u);
+            uint32_t hr = tseed ^ (0x9E3779B9u * (idx + 1u));   // mix32 (lowbias32)
             hr ^= hr >> 16;
             hr *= 0x7FEB352Du;
             hr ^= hr >> 15;
