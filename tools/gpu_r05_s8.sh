@@ -1,16 +1,19 @@
 #!/bin/bash
-# r05 step 8: counter list of the box, then SQ / GRBM / TA counters of the generator (split kernel)
-# at the configs[3] chunk shape, one counter set per process under its own kill timeout.
+# r05 step 8: SQ / TA / TD / TCP / TCC counters of the generator's keys kernel at the configs[3]
+# chunk shape (product library, or POPBAM_GPU_LIB), one counter set per process under its own
+# kill timeout.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R"; O=gpurun_out/r05s8; mkdir -p $O/pmc; export TMPDIR=/tmp
-timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || echo "counter list failed"
+cd "$R"; O=gpurun_out/r05s8${TAG:-}; rm -rf $O; mkdir -p $O/pmc; export TMPDIR=/tmp
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" \
            "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC" \
-           "GRBM_GUI_ACTIVE GRBM_COUNT" "TA_TA_BUSY TA_BUFFER_WAVEFRONTS" "TA_BUFFER_READ_WAVEFRONTS TA_BUFFER_WRITE_WAVEFRONTS" \
-           "TD_TD_BUSY TD_TC_STALL"; do
+           "GRBM_GUI_ACTIVE GRBM_COUNT" "TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum" "TD_TD_BUSY_sum TD_TC_STALL_sum" \
+           "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_WRITE_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum" \
+           "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_PENDING_STALL_CYCLES_sum TCP_UTCL1_STALL_INFLIGHT_MAX_sum" \
+           "TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_WRITE_TAGCONFLICT_STALL_CYCLES_sum" \
+           "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $set -T --output-format csv -d "$R/$O/pmc/p$i" -o run \
     -- python3 "$R/tools/synth_bench.py" --samples 24 --sites 33554432 --reps 2 > $O/pmc/p$i.log 2>&1 || { echo "pmc pass $i ($set) failed"; tail -3 $O/pmc/p$i.log; }
 done
-python3 tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt; grep -A60 "^synth_keys_split_kernel" $O/pmc_summary.txt | head -70
+python3 tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt; grep -A60 "^synth_keys_fast_kernel" $O/pmc_summary.txt | head -70
