@@ -1209,9 +1209,12 @@ extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int3
         depth[s] = (uint16_t)d;
         int a0 = (snp && (uint32_t)(hs & 0xFFFF) < f16) ? alt : ref_idx;
         int a1 = (snp && (uint32_t)((hs >> 16) & 0xFFFF) < f16) ? alt : ref_idx;
-        // read r = template entry base + 8 (s + n (r >> 3)) + (r & 7), base a multiple of 64 from
-        // bits 32..45 of the site hash (pbg_common.h synth_tmpl_base / synth_tmpl_index / _entry)
-        const uint32_t base = (uint32_t)((h >> 32) & ((1u << 14) - 1)) * 64u;
+        // read r = template entry base + 8 (s + n (r >> 3)) + (r & 7): base = the page of the
+        // position's 16,384-position span + 64 x bits 32..37 of the site hash (pbg_common.h
+        // synth_tmpl_page / synth_tmpl_base / synth_tmpl_index / synth_tmpl_entry)
+        const uint64_t span = (pos >> 14) | ((uint64_t)(uint32_t)contig << 40);
+        const uint32_t page = (uint32_t)(sm64(seed ^ 0x243F6A8885A308D3ULL ^ span) & ((1u << 20) / 4096u - 1u)) * 4096u;
+        const uint32_t base = page + (uint32_t)((h >> 32) & 63u) * 64u;
         for (int r = 0; r < d; ++r) {
             const uint32_t idx = base + 8u * ((uint32_t)s + (uint32_t)n * ((uint32_t)r >> 3)) + ((uint32_t)r & 7u);
             uint32_t hr = tseed ^ (0x9E3779B9u * (idx + 1u));   // mix32 (lowbias32)

@@ -160,17 +160,23 @@ __host__ __device__ inline int synth_depth(uint64_t hs, int mean_depth) {
     const uint64_t m = nb >= 64 ? ~0ULL : ((1ULL << nb) - 1);
     return __builtin_popcountll(((uint64_t)b0 | ((uint64_t)b1 << 32)) & m);
 }
-// The per-read draws come from a table of read templates (kTmplN entries + a tail, 2 MB as u16,
-// L2-resident).  A position's samples read interleaved 8-entry chunks of one window starting at
-// synth_tmpl_base(site hash), a random multiple of 64: read r of sample s (of n) is entry
+// The per-read draws come from a table of read templates (kTmplN entries + a tail, 2 MB as u16).
+// Positions come in spans of 16,384 (absolute position >> 14); a span draws its windows from one
+// page of the table, kTmplPage entries at synth_tmpl_page(seed, contig, pos), and a position's
+// window starts at a random multiple of 64 in that page (synth_tmpl_base: 64 starts a page, 16 K
+// over the table, as many as a window anywhere in the table would have).  Its samples read
+// interleaved 8-entry chunks of the window: read r of sample s (of n) is entry
 // base + 8 (s + n (r >> 3)) + (r & 7) (synth_tmpl_index).  Distinct samples read distinct
-// entries, and chunk c of a position's consecutive samples is one contiguous run, so the
-// generator's 16-byte template loads of a wave's tasks coalesce (r05; a window per task at a
-// random place had cost a cache line per lane and load).  Entry i: bq << 5 | strand << 4 |
+// entries; chunk c of a position's consecutive samples is one contiguous run (coalesced loads);
+// and a workgroup of consecutive positions finds every read it needs in one page plus the
+// window's reach, which fits LDS (r05: the keys kernel reads its templates from LDS, not through
+// the vector cache it writes 16 GB a chunk through).  Entry i: bq << 5 | strand << 4 |
 // hap << 2 | e, drawn from 32 random bits hr_i: haplotype (bit 0), error (bits 1-7 all zero:
 // 1/128) with the error base 1..3 steps away (e, from bits 8-15; e = 0: no error), baseQ 20..40
 // (bits 16-31), strand (bit 8 ^ bit 17).  Fixed-point ranges, no division.
 constexpr uint32_t kTmplN = 1u << 20;
+constexpr uint32_t kTmplPage = 4096;            // entries whose 64-entry steps a page's windows start at
+constexpr int kTmplSpanShift = 14;              // positions share a page in spans of 16,384
 constexpr uint32_t kTmplSize = kTmplN + 8192;   // a window reaches base + 8 (125 + 126 * 7) + 8 (64 reads, 126 samples)
 __host__ __device__ inline uint32_t synth_tmpl_seed(uint64_t seed) {
     return (uint32_t)splitmix64(seed ^ 0x6A09E667F3BCC909ULL);
@@ -182,8 +188,16 @@ __host__ __device__ inline uint32_t synth_tmpl_entry(uint32_t tseed, uint32_t i)
     const uint32_t strand = ((hr >> 8) ^ (hr >> 17)) & 1u;
     return (bq << 5) | (strand << 4) | ((hr & 1u) << 2) | e;
 }
-// a position's template window (bits 32..45 of its site hash; the site fields use bits 0..31)
-__host__ __device__ inline uint32_t synth_tmpl_base(uint64_t h) { return (uint32_t)((h >> 32) & (kTmplN / 64 - 1)) * 64u; }
+// the page of a position's span: a multiple of kTmplPage in [0, kTmplN)
+__host__ __device__ inline uint32_t synth_tmpl_page(uint64_t seed, int contig, uint64_t pos) {
+    const uint64_t span = (pos >> kTmplSpanShift) | ((uint64_t)(uint32_t)contig << 40);
+    return (uint32_t)(splitmix64(seed ^ 0x243F6A8885A308D3ULL ^ span) & (kTmplN / kTmplPage - 1)) * kTmplPage;
+}
+// a position's template window: its span's page + 64 x (bits 32..37 of its site hash; the site
+// fields use bits 0..31)
+__host__ __device__ inline uint32_t synth_tmpl_base(uint64_t h, uint32_t page) {
+    return page + (uint32_t)((h >> 32) & (kTmplPage / 64 - 1)) * 64u;
+}
 // template entry of read r of sample s (of n) at a position with window base
 __host__ __device__ inline uint32_t synth_tmpl_index(uint32_t base, uint32_t n, uint32_t s, uint32_t r) {
     return base + 8u * (s + n * (r >> 3)) + (r & 7u);
@@ -199,10 +213,11 @@ __host__ __device__ inline uint32_t synth_tmpl_read(uint32_t ent, uint32_t alv) 
     const uint32_t base = (((alv >> (2u * ((ent >> 2) & 1u))) & 3u) + (ent & 3u)) & 3u;
     return (ent >> 5) | (60u << 8) | ((1u << base) << 16) | (((ent >> 4) & 1u) << 20);
 }
-// read r of sample `sample` (of n) at a site
-__host__ __device__ inline uint32_t synth_read(const SynthSite &s, uint64_t hs, int n, int sample, int r, uint32_t tseed) {
-    return synth_tmpl_read(synth_tmpl_entry(tseed, synth_tmpl_index(synth_tmpl_base(s.h), (uint32_t)n, (uint32_t)sample,
-                                                                    (uint32_t)r)),
+// read r of sample `sample` (of n) at a site whose span's page is `page`
+__host__ __device__ inline uint32_t synth_read(const SynthSite &s, uint64_t hs, uint32_t page, int n, int sample, int r,
+                                               uint32_t tseed) {
+    return synth_tmpl_read(synth_tmpl_entry(tseed, synth_tmpl_index(synth_tmpl_base(s.h, page), (uint32_t)n,
+                                                                    (uint32_t)sample, (uint32_t)r)),
                            synth_alleles(s, hs));
 }
 // every synthetic read survives call_base's filters: baseQ 20..40 (no Illumina offset), mapQ 60,

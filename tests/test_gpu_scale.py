@@ -25,32 +25,38 @@ def _ctx(n, n_pops=2, **kw):
 SHAPES = [(12, 2), (24, 2), (24, 3), (30, 3), (48, 2), (62, 2), (64, 4), (96, 3), (126, 2)]
 
 
-@pytest.mark.parametrize("n,kw,contig", [(12, {}, 0), (12, {}, 3), (24, {"flag": 0x02}, 0),
-                                          (40, {"min_baseQ": 30, "min_mapQ": 61}, 1),
-                                          (64, {"max_depth": 12, "min_depth": 8}, 0), (5, {"max_depth": 300}, 2),
-                                          (96, {}, 1)])
-def test_synthetic_generator_matches_oracle(gpu_lib, n, kw, contig):
+# pos0 1000: template-page span borders inside the keys kernel's 512-position workgroups (the
+# straddle launch); 3 * 2^14 - 320: ditto, a border 320 positions in; 2^33: no border inside a
+# workgroup (pos0 a multiple of 512), positions past 32 bits
+@pytest.mark.parametrize("n,kw,contig,pos0", [(12, {}, 0, 1000), (12, {}, 3, 1000), (24, {"flag": 0x02}, 0, 1000),
+                                               (40, {"min_baseQ": 30, "min_mapQ": 61}, 1, 1000),
+                                               (64, {"max_depth": 12, "min_depth": 8}, 0, 1000),
+                                               (5, {"max_depth": 300}, 2, 1000), (96, {}, 1, 1000),
+                                               (24, {}, 0, 3 * 16384 - 320), (24, {}, 1, 1 << 33),
+                                               (126, {}, 0, 1 << 33)])
+def test_synthetic_generator_matches_oracle(gpu_lib, n, kw, contig, pos0):
     """pbg_synth_pileup = the oracle's raw generator + the host packer (call_base's per-read
-    loop, libpopbam_feed.so), for every filter variant, k width and contig key."""
+    loop, libpopbam_feed.so), for every filter variant, k width, contig key and kind of
+    start position."""
     import torch
     from popbam_amd import workload
     ctx, params = _ctx(n, **kw)
     nsites = 64 * 2000 + 17
-    syn = workload.SynthPileup(ctx, nsites, 10, SEED, contig=contig, pos0=1000)
+    syn = workload.SynthPileup(ctx, nsites, 10, SEED, contig=contig, pos0=pos0)
     kt = np.uint8 if ctx.k_bytes == 1 else np.uint16
     k = syn.k.cpu().numpy().view(kt).reshape(-1, n)
     rq = syn.rmsq.cpu().numpy().view(np.uint32).reshape(-1, n)
     boff = syn.block_off.cpu().numpy()
     keys = syn.keys.cpu().numpy().view(np.uint16)
     ref = syn.ref.cpu().numpy()
-    cpu = harness.key_batch(harness.synth_batch(SEED, 1000, 1000 + nsites, n, 10, params.max_depth, contig), params)
+    cpu = harness.key_batch(harness.synth_batch(SEED, pos0, pos0 + nsites, n, 10, params.max_depth, contig), params)
     assert np.array_equal(ref, cpu["ref"])
     assert np.array_equal(k, cpu["k"])
     assert np.array_equal(rq, cpu["rmsq"])
     assert np.array_equal(boff, cpu["block_off"])
     assert syn.n_keys == len(cpu["keys"]) and np.array_equal(keys[:syn.n_keys], cpu["keys"])
     # pipelined form: worst-case keys_cap, no host sync
-    syn2 = workload.SynthPileup(ctx, nsites, 10, SEED, contig=contig, pos0=1000, keys_cap=syn.max_keys)
+    syn2 = workload.SynthPileup(ctx, nsites, 10, SEED, contig=contig, pos0=pos0, keys_cap=syn.max_keys)
     assert np.array_equal(syn2.keys.cpu().numpy().view(np.uint16)[:syn.n_keys], cpu["keys"])
     # too small a keys[]: flagged, nothing written past it
     from popbam_amd import _lib
