@@ -1214,9 +1214,18 @@ extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int3
         // synth_tmpl_page / synth_tmpl_base / synth_tmpl_index / synth_tmpl_entry)
         const uint64_t span = (pos >> 14) | ((uint64_t)(uint32_t)contig << 40);
         const uint32_t page = (uint32_t)(sm64(seed ^ 0x243F6A8885A308D3ULL ^ span) & ((1u << 20) / 4096u - 1u)) * 4096u;
-        const uint32_t base = page + (uint32_t)((h >> 32) & 63u) * 64u;
+        const uint32_t wbase = page + (uint32_t)((h >> 32) & 63u) * 64u;
+        // the task's errors (pbg_common.h synth_errors): at most two reads, P(one) = d / 128,
+        // P(two) = d (d - 1) / 32768, from one hash of the sample hash's lower half
+        const uint32_t du = (uint32_t)d, eh = mx32((uint32_t)hs ^ 0x2545F491u);
+        const uint32_t eu = eh & 0x3FFFu, p2 = (du * (du > 0u ? du - 1u : 0u)) >> 1, p1 = du << 7;
+        const uint32_t ne = eu < p2 ? 2u : (eu < p2 + p1 ? 1u : 0u);
+        const uint32_t j1 = (((eh >> 14) & 63u) * du) >> 6;
+        uint32_t j2 = j1 + 1u + (du > 1u ? (((eh >> 20) & 63u) * (du - 1u)) >> 6 : 0u);
+        if (j2 >= du) j2 -= du;
+        const uint32_t e1 = 1u + ((((eh >> 26) & 7u) * 3u) >> 3), e2 = 1u + ((((eh >> 29) & 7u) * 3u) >> 3);
         for (int r = 0; r < d; ++r) {
-            const uint32_t idx = base + 8u * ((uint32_t)s + (uint32_t)n * ((uint32_t)r >> 3)) + ((uint32_t)r & 7u);
+            const uint32_t idx = wbase + 8u * ((uint32_t)s + (uint32_t)n * ((uint32_t)r >> 3)) + ((uint32_t)r & 7u);
             uint32_t hr = tseed ^ (0x9E3779B9u * (idx + 1u));   // mix32 (lowbias32)
             hr ^= hr >> 16;
             hr *= 0x7FEB352Du;
@@ -1224,7 +1233,8 @@ extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int3
             hr *= 0x846CA68Bu;
             hr ^= hr >> 16;
             int base = (hr & 1) ? a1 : a0;
-            if (((hr >> 1) & 127) == 0) base = (base + 1 + (int)((((hr >> 8) & 0xFFu) * 3u) >> 8)) & 3;
+            if (ne >= 1u && (uint32_t)r == j1) base = (base + (int)e1) & 3;
+            if (ne >= 2u && (uint32_t)r == j2) base = (base + (int)e2) & 3;
             uint32_t bq = 20 + ((((hr >> 16) & 0xFFFFu) * 21u) >> 16);
             uint32_t strand = ((hr >> 8) ^ (hr >> 17)) & 1u;
             if (reads) reads[nr] = bq | (60u << 8) | ((1u << base) << 16) | (strand << 20);

@@ -170,10 +170,12 @@ __host__ __device__ inline int synth_depth(uint64_t hs, int mean_depth) {
 // entries; chunk c of a position's consecutive samples is one contiguous run (coalesced loads);
 // and a workgroup of consecutive positions finds every read it needs in one page plus the
 // window's reach, which fits LDS (r05: the keys kernel reads its templates from LDS, not through
-// the vector cache it writes 16 GB a chunk through).  Entry i: bq << 5 | strand << 4 |
-// hap << 2 | e, drawn from 32 random bits hr_i: haplotype (bit 0), error (bits 1-7 all zero:
-// 1/128) with the error base 1..3 steps away (e, from bits 8-15; e = 0: no error), baseQ 20..40
-// (bits 16-31), strand (bit 8 ^ bit 17).  Fixed-point ranges, no division.
+// the vector cache it writes 16 GB a chunk through).  Entry i: bq << 5 | strand << 4 | hap << 2,
+// drawn from 32 random bits hr_i: haplotype (bit 0), baseQ 20..40 (bits 16-31), strand (bit 8 ^
+// bit 17).  Fixed-point ranges, no division.  Sequencing errors are the task's own
+// (synth_errors), not the template's: positions that share a page would otherwise share its
+// errors, and the spurious segregating sites two errors in one sample make would cluster by
+// span (a 10 kb window's count: sd 120 against 16 with the errors drawn per task).
 constexpr uint32_t kTmplN = 1u << 20;
 constexpr uint32_t kTmplPage = 4096;            // entries whose 64-entry steps a page's windows start at
 constexpr int kTmplSpanShift = 14;              // positions share a page in spans of 16,384
@@ -183,10 +185,9 @@ __host__ __device__ inline uint32_t synth_tmpl_seed(uint64_t seed) {
 }
 __host__ __device__ inline uint32_t synth_tmpl_entry(uint32_t tseed, uint32_t i) {
     const uint32_t hr = mix32(tseed ^ (0x9E3779B9u * (i + 1u)));
-    const uint32_t e = ((hr >> 1) & 127u) == 0 ? 1u + ((((hr >> 8) & 0xFFu) * 3u) >> 8) : 0u;
     const uint32_t bq = 20u + ((((hr >> 16) & 0xFFFFu) * 21u) >> 16);
     const uint32_t strand = ((hr >> 8) ^ (hr >> 17)) & 1u;
-    return (bq << 5) | (strand << 4) | ((hr & 1u) << 2) | e;
+    return (bq << 5) | (strand << 4) | ((hr & 1u) << 2);
 }
 // the page of a position's span: a multiple of kTmplPage in [0, kTmplN)
 __host__ __device__ inline uint32_t synth_tmpl_page(uint64_t seed, int contig, uint64_t pos) {
@@ -208,17 +209,42 @@ __host__ __device__ inline uint32_t synth_alleles(const SynthSite &s, uint64_t h
     const int a1 = (s.snp && (uint32_t)((hs >> 16) & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
     return (uint32_t)(a0 | (a1 << 2));
 }
+// A task's sequencing errors: at most two of its d reads (d <= 64), P(one) = d / 128,
+// P(two) = d (d - 1) / 32768 -- the binomial's first two terms at 1/128 a read -- at distinct
+// reads j1, j2, each read's base moved e1, e2 in 1..3 steps (weights 3/8, 3/8, 2/8), all from one
+// hash of the sample hash's lower half.
+struct SynthErr {
+    uint32_t ne, j1, j2, e1, e2;
+};
+__host__ __device__ inline SynthErr synth_errors(uint32_t hs_lo, uint32_t d) {
+    const uint32_t eh = mix32(hs_lo ^ 0x2545F491u);
+    const uint32_t u = eh & 0x3FFFu;                                  // in 1 / 16384
+    const uint32_t p2 = (d * (d > 0u ? d - 1u : 0u)) >> 1, p1 = d << 7;
+    SynthErr e;
+    e.ne = u < p2 ? 2u : (u < p2 + p1 ? 1u : 0u);
+    e.j1 = (((eh >> 14) & 63u) * d) >> 6;
+    uint32_t j2 = e.j1 + 1u + (d > 1u ? (((eh >> 20) & 63u) * (d - 1u)) >> 6 : 0u);
+    e.j2 = j2 >= d ? j2 - d : j2;
+    e.e1 = 1u + ((((eh >> 26) & 7u) * 3u) >> 3);
+    e.e2 = 1u + ((((eh >> 29) & 7u) * 3u) >> 3);
+    return e;
+}
+// the error base offset of read r (0: none)
+__host__ __device__ inline uint32_t synth_err_off(const SynthErr &e, uint32_t r) {
+    return (e.ne >= 1u && r == e.j1 ? e.e1 : 0u) + (e.ne >= 2u && r == e.j2 ? e.e2 : 0u);
+}
 // raw read word (bits 0-7 baseQ, 8-15 mapQ 60, 16-19 nt16 base, 20 strand) of a template entry
+// with the read's error offset in bits 0-1 (the entry's own are zero)
 __host__ __device__ inline uint32_t synth_tmpl_read(uint32_t ent, uint32_t alv) {
     const uint32_t base = (((alv >> (2u * ((ent >> 2) & 1u))) & 3u) + (ent & 3u)) & 3u;
     return (ent >> 5) | (60u << 8) | ((1u << base) << 16) | (((ent >> 4) & 1u) << 20);
 }
-// read r of sample `sample` (of n) at a site whose span's page is `page`
-__host__ __device__ inline uint32_t synth_read(const SynthSite &s, uint64_t hs, uint32_t page, int n, int sample, int r,
-                                               uint32_t tseed) {
-    return synth_tmpl_read(synth_tmpl_entry(tseed, synth_tmpl_index(synth_tmpl_base(s.h, page), (uint32_t)n,
-                                                                    (uint32_t)sample, (uint32_t)r)),
-                           synth_alleles(s, hs));
+// read r of sample `sample` (of n, depth d) at a site whose span's page is `page`
+__host__ __device__ inline uint32_t synth_read(const SynthSite &s, uint64_t hs, uint32_t page, int n, int sample, int d,
+                                               int r, uint32_t tseed) {
+    const uint32_t ent = synth_tmpl_entry(tseed, synth_tmpl_index(synth_tmpl_base(s.h, page), (uint32_t)n,
+                                                                   (uint32_t)sample, (uint32_t)r));
+    return synth_tmpl_read(ent | synth_err_off(synth_errors((uint32_t)hs, (uint32_t)d), (uint32_t)r), synth_alleles(s, hs));
 }
 // every synthetic read survives call_base's filters: baseQ 20..40 (no Illumina offset), mapQ 60,
 // one-hot A/C/G/T bases
