@@ -1215,10 +1215,12 @@ extern "C" void orc_synth_site(uint64_t seed, int32_t contig, uint64_t pos, int3
         const uint64_t span = (pos >> 14) | ((uint64_t)(uint32_t)contig << 40);
         const uint32_t page = (uint32_t)(sm64(seed ^ 0x243F6A8885A308D3ULL ^ span) & ((1u << 20) / 4096u - 1u)) * 4096u;
         const uint32_t wbase = page + (uint32_t)((h >> 32) & 63u) * 64u;
-        // the task's errors (pbg_common.h synth_errors): at most two reads, P(one) = d / 128,
-        // P(two) = d (d - 1) / 32768, from one hash of the sample hash's lower half
+        // the task's errors (pbg_common.h synth_errors): at most two reads, P(one) =
+        // d/128 (1 - (d-1)/128), P(two) = d (d - 1) / 32768 (1 - (d-2)/128), from one hash of the
+        // sample hash's lower half
         const uint32_t du = (uint32_t)d, eh = mx32((uint32_t)hs ^ 0x2545F491u);
-        const uint32_t eu = eh & 0x3FFFu, p2 = (du * (du > 0u ? du - 1u : 0u)) >> 1, p1 = du << 7;
+        const uint32_t dd1 = du * (du > 0u ? du - 1u : 0u);
+        const uint32_t eu = eh & 0x3FFFu, p2 = (dd1 * (130u - du)) >> 8, p1 = (du << 7) - dd1;
         const uint32_t ne = eu < p2 ? 2u : (eu < p2 + p1 ? 1u : 0u);
         const uint32_t j1 = (((eh >> 14) & 63u) * du) >> 6;
         uint32_t j2 = j1 + 1u + (du > 1u ? (((eh >> 20) & 63u) * (du - 1u)) >> 6 : 0u);

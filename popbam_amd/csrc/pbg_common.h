@@ -209,8 +209,9 @@ __host__ __device__ inline uint32_t synth_alleles(const SynthSite &s, uint64_t h
     const int a1 = (s.snp && (uint32_t)((hs >> 16) & 0xFFFF) < s.f16) ? s.alt : s.ref_idx;
     return (uint32_t)(a0 | (a1 << 2));
 }
-// A task's sequencing errors: at most two of its d reads (d <= 64), P(one) = d / 128,
-// P(two) = d (d - 1) / 32768 -- the binomial's first two terms at 1/128 a read -- at distinct
+// A task's sequencing errors: at most two of its d reads (d <= 64), P(one) = d/128 (1 - (d-1)/128),
+// P(two) = d (d - 1) / 32768 (1 - (d-2)/128) -- the binomial's first two terms at 1/128 a read, to
+// first order -- at distinct
 // reads j1, j2, each read's base moved e1, e2 in 1..3 steps (weights 3/8, 3/8, 2/8), all from one
 // hash of the sample hash's lower half.
 struct SynthErr {
@@ -219,7 +220,8 @@ struct SynthErr {
 __host__ __device__ inline SynthErr synth_errors(uint32_t hs_lo, uint32_t d) {
     const uint32_t eh = mix32(hs_lo ^ 0x2545F491u);
     const uint32_t u = eh & 0x3FFFu;                                  // in 1 / 16384
-    const uint32_t p2 = (d * (d > 0u ? d - 1u : 0u)) >> 1, p1 = d << 7;
+    const uint32_t dd1 = d * (d > 0u ? d - 1u : 0u);
+    const uint32_t p2 = (dd1 * (130u - d)) >> 8, p1 = (d << 7) - dd1;
     SynthErr e;
     e.ne = u < p2 ? 2u : (u < p2 + p1 ? 1u : 0u);
     e.j1 = (((eh >> 14) & 63u) * d) >> 6;

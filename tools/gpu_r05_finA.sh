@@ -1,0 +1,10 @@
+#!/bin/bash
+# r05 final A: the whole -m gpu suite, then smoke.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; O=gpurun_out/r05finA; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 \
+    --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log; tail -3 $O/pytest_gpu.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
