@@ -1,7 +1,7 @@
 #!/bin/bash
-# r05 step 13: configs[2] bench, product vs a variant library, alternating (run-order balanced).
+# configs[2] bench, product vs a variant library, alternating (run-order balanced).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R"; O=gpurun_out/r05s13; mkdir -p $O; export TMPDIR=/tmp
+cd "$R"; O=gpurun_out/bench_ab; mkdir -p $O; export TMPDIR=/tmp
 for rep in 1 2; do
 for v in product ${AB:-}; do
   L=""; [ "$v" != product ] && L=$R/popbam_amd/variants/$v/libpopbam_gpu.so

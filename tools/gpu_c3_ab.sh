@@ -1,7 +1,7 @@
 #!/bin/bash
-# r05 step 10: configs[3] window stage, product vs a variant library (POPBAM_GPU_LIB).
+# configs[3] window stage, product vs a variant library (POPBAM_GPU_LIB).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R"; O=gpurun_out/r05s10; mkdir -p $O; export TMPDIR=/tmp
+cd "$R"; O=gpurun_out/c3_ab; mkdir -p $O; export TMPDIR=/tmp
 for v in product ${AB:-}; do
   L=""; [ "$v" != product ] && L=$R/popbam_amd/variants/$v/libpopbam_gpu.so
   POPBAM_GPU_LIB=$L timeout -k 10 300 python bench.py --config 3 --steps 1 --warmup 1 --cpu-sample 0 > $O/$v.json 2> $O/$v.err || { tail -5 $O/$v.err; exit 1; }

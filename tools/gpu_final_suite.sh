@@ -1,7 +1,7 @@
 #!/bin/bash
-# r05 final A: the whole -m gpu suite, then smoke.
+# Round-end check: the whole -m gpu suite, then smoke.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R"; O=gpurun_out/r05finA; mkdir -p $O; export TMPDIR=/tmp
+cd "$R"; O=gpurun_out/final; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 \
     --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log; tail -3 $O/pytest_gpu.log

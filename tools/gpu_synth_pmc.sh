@@ -1,9 +1,9 @@
 #!/bin/bash
-# r05 step 8: SQ / TA / TD / TCP / TCC counters of the generator's keys kernel at the configs[3]
+# SQ / TA / TD / TCP / TCC counters of the generator's keys kernel at the configs[3]
 # chunk shape (product library, or POPBAM_GPU_LIB), one counter set per process under its own
 # kill timeout.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R"; O=gpurun_out/r05s8${TAG:-}; rm -rf $O; mkdir -p $O/pmc; export TMPDIR=/tmp
+cd "$R"; O=gpurun_out/synth_pmc${TAG:-}; rm -rf $O; mkdir -p $O/pmc; export TMPDIR=/tmp
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" \
            "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC" \
