@@ -100,7 +100,7 @@ def parse():
     ap.add_argument("--step", type=int, default=500, help="config 4: window step (overlapping windows)")
     ap.add_argument("--contigs", type=int, default=24, help="config 3: contigs")
     ap.add_argument("--contig-len", type=int, default=125_000_000, help="config 3: positions per contig")
-    ap.add_argument("--chunk", type=int, default=1 << 25, help="config 3: positions per streamed pileup chunk")
+    ap.add_argument("--chunk", type=int, default=1 << 25, help="configs[3]/[4]: positions per streamed pileup chunk (default 2^27 serial or 2^25 --overlap / 2^23)")
     ap.add_argument("--overlap", action="store_true",
                     help="configs[3]/[4]: generate chunk c+1 on a second stream beside the call of chunk c "
                          "(default: generate then call on one stream, so the call kernels run alone)")
@@ -109,6 +109,8 @@ def parse():
                          "statistics on a second stream beside the next piece's call (1 = call, then statistics)")
     args = ap.parse_args()
     if args.config == 3:
+        if args.chunk == 1 << 25 and not args.overlap:
+            args.chunk = 1 << 27   # one chunk per 125 Mbp contig: ~64 GB of keys in the one serial buffer
         if args.samples == 12:
             args.samples = 24
         if args.seed == 0xC0FFEE02:
