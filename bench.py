@@ -100,7 +100,13 @@ def parse():
     ap.add_argument("--step", type=int, default=500, help="config 4: window step (overlapping windows)")
     ap.add_argument("--contigs", type=int, default=24, help="config 3: contigs")
     ap.add_argument("--contig-len", type=int, default=125_000_000, help="config 3: positions per contig")
-    ap.add_argument("--chunk", type=int, default=1 << 25, help="configs[3]/[4]: positions per streamed pileup chunk (default 2^27 serial or 2^25 --overlap / 2^23)")
+    ap.add_argument("--chunk", type=int, default=None, help="configs[3]/[4]: positions per streamed pileup chunk (default 2^27 serial or 2^25 --overlap / 2^23)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: each rank builds its shard plan, joins the gloo barrier / max-over-ranks timing "
+                         "and rank 0 prints the line with value null (tests the --gpus N launch on CPU)")
+    ap.add_argument("--allow-variant", action="store_true",
+                    help="accept a library whose pbg_build_info() is not 'product' (bounds / experiment builds); "
+                         "the line then says so in build.kind and is not a product measurement")
     ap.add_argument("--overlap", action="store_true",
                     help="configs[3]/[4]: generate chunk c+1 on a second stream beside the call of chunk c "
                          "(default: generate then call on one stream, so the call kernels run alone)")
@@ -108,9 +114,13 @@ def parse():
                     help="config 2: the contig's call in this many pieces (window borders), each piece's "
                          "statistics on a second stream beside the next piece's call (1 = call, then statistics)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.chunk is None:
+        # one chunk per 125 Mbp contig (~64 GB of keys in the one serial buffer) for configs[3]'s
+        # serial pass, 2^25 when two buffers alternate (--overlap), 2^23 at configs[4]'s 96 samples
+        args.chunk = {3: (1 << 25) if args.overlap else (1 << 27), 4: 1 << 23}.get(args.config, 1 << 25)
     if args.config == 3:
-        if args.chunk == 1 << 25 and not args.overlap:
-            args.chunk = 1 << 27   # one chunk per 125 Mbp contig: ~64 GB of keys in the one serial buffer
         if args.samples == 12:
             args.samples = 24
         if args.seed == 0xC0FFEE02:
@@ -124,8 +134,6 @@ def parse():
             args.window = 1000
         if args.contig_len == 125_000_000:
             args.contig_len = 200_000_000
-        if args.chunk == 1 << 25:
-            args.chunk = 1 << 23   # 96 samples: ~16 GB of keys per chunk buffer
         args.contigs = 1
     return args
 
@@ -609,7 +617,7 @@ def max_over_ranks(dist, x: float) -> float:
     return float(t.item())
 
 
-def bench_genome(args, torch, dist, world, rank):
+def bench_genome(args, torch, dist, world, rank, binfo):
     """configs[3]: the whole synthetic genome (contigs x contig-len, 24 samples) streamed through
     HBM in double-buffered pileup chunks (popbam_amd.genome), contig-first shards across ranks,
     nucdiv + sfs + ld (ZnS) + diverge over 10 kb windows.  Strong scaling: the genome is fixed."""
@@ -738,38 +746,153 @@ def bench_genome(args, torch, dist, world, rank):
             out["parity_sample"] = ps
             out["rows_crosscheck"] = xcheck
         out["src_sha"] = source_hash()
+        out["build"] = binfo
         print(json.dumps(out), flush=True)
     ctx.close()
 
 
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) run without a launcher: start N rank processes of this script, one per
+    GPU, with the environment torch.distributed.run gives its workers (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT).  This process imports neither torch nor
+    the library and never touches HIP; the ranks are children (subprocess), not an exec.  They
+    inherit stdout, and only rank 0 prints the line.  Returns the first failing rank's status (the
+    others are then terminated, so none is left waiting in a barrier), 0 when all succeed."""
+    import socket
+    import subprocess
+    n = args.gpus
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0")
+    argv = [sys.executable, os.path.abspath(__file__), *sys.argv[1:]]
+    procs = [subprocess.Popen(argv, env=dict(base, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad and rc == 0:
+                rc = bad[0]
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+            time.sleep(0.1)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    return 0 if rc == 0 else (rc if rc > 0 else 1)
+
+
+def init_gloo(world: int):
+    """gloo (host) process group for the timing barrier and the max over ranks: the data path
+    has no collective, so RCCL is never initialised.  gloo announces its peer connections on
+    stdout: they are kept off the one JSON line."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo")
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+    return dist
+
+
+def dry_run(args, world: int, rank: int):
+    """--dry-run: the multi-rank launch and the shard plan without a GPU.  Each rank builds its
+    shard (configs[2]: its own contig of --sites positions; configs[3]/[4]: genome.rank_plan),
+    joins the same barrier + max-over-ranks timing as a real run, and rank 0 prints the line
+    with `value` null, every rank's positions / windows, and whether the ranks' windows cover
+    the workload exactly once."""
+    dist = init_gloo(world)
+    if os.environ.get("BENCH_DRY_FAIL_RANK") == str(rank):   # tests: a rank that dies before the barrier
+        sys.exit(3)
+    from popbam_amd import genome, workload
+    if args.config == 2:
+        mine = {"rank": rank, "sites": args.sites, "windows": len(workload.reference_windows(0, args.sites, args.window))}
+        want_windows = mine["windows"] * world
+    else:
+        lengths = [args.contig_len] * args.contigs
+        segs, _ = genome.rank_plan(args.config, lengths, world, rank, args.window, args.step)
+        if args.config == 4:
+            nw = sum(len(range(s.win_lo, s.win_hi, s.step)) for s in segs)
+            want_windows = max(0, (args.contig_len - args.window) // args.step + 1)
+        else:
+            nw = sum(len(genome.contig_windows(args.contig_len, args.window, s.beg, s.end)) for s in segs)
+            want_windows = sum(len(genome.contig_windows(L, args.window)) for L in lengths)
+        mine = {"rank": rank, "sites": sum(s.end - s.beg for s in segs), "windows": nw, "segments": len(segs)}
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    ranks = [None] * world
+    if dist:
+        dist.all_gather_object(ranks, mine)
+    else:
+        ranks = [mine]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Msites/s", "n_gpus": world, "steps": 0,
+                          "warmup": 0, "ms_per_step": None, "higher_is_better": True,
+                          "scaling": "weak" if args.config == 2 else "strong", "vs_baseline": None, "dtype": "f64",
+                          "data": "none (dry run: no GPU, no compute)", "dry_run": True,
+                          "barrier_s": round(elapsed, 6), "config": {"workload": f"configs[{args.config}] shard plan",
+                                                                     "parallelism": f"dp{world}"},
+                          "ranks": ranks, "windows_covered": sum(r["windows"] for r in ranks) == want_windows}),
+              flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def build_info(allow_variant: bool) -> dict:
+    """Which libpopbam_gpu.so this run measures (path and pbg_build_info(): 'product', 'bounds' or
+    'experiment').  A non-product build (tools/variant.sh, a PBG_BOUNDS build; some give wrong
+    results) is refused unless --allow-variant, and then the line carries its kind."""
+    from popbam_amd import _lib
+    kind = _lib.load().pbg_build_info().decode()
+    info = {"kind": kind, "library": os.path.relpath(_lib.LIB_PATH, REPO) if _lib.LIB_PATH.startswith(REPO)
+            else _lib.LIB_PATH}
+    if kind != "product" and not allow_variant:
+        sys.exit(f"bench.py: {info['library']} is a '{kind}' build, not the product (pass --allow-variant to "
+                 "measure it anyway; the line then records build.kind)")
+    return info
+
+
 def main():
     args = parse()
-    import torch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} from the launcher but --gpus {args.gpus}: they must agree")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
+    import torch
+
     dist = None
+    binfo = build_info(args.allow_variant)
     if world > 1:
-        # gloo (host) for the timing barrier and the max over ranks: the data path has no
-        # collective, so RCCL is never initialised
-        import torch.distributed as dist
         # one rank per GPU; more ranks than GPUs (a rehearsal on a smaller box) share them
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-        # gloo announces its peer connections on stdout: keep them off the one JSON line
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
-            dist.init_process_group("gloo")
-        finally:
-            os.dup2(saved, 1)
-            os.close(saved)
+        dist = init_gloo(world)
     else:
         torch.cuda.set_device(0)
 
     if args.config in (3, 4):
-        bench_genome(args, torch, dist, world, rank)
+        bench_genome(args, torch, dist, world, rank, binfo)
         if dist:
             dist.destroy_process_group()
         return
@@ -896,6 +1019,7 @@ def main():
             out["parity_sample"] = ps
             out["rows_crosscheck"] = rows_crosscheck(torch, ctx, hp)
         out["src_sha"] = source_hash()
+        out["build"] = binfo
         print(json.dumps(out), flush=True)
     ctx.check(ctx.lib.pbg_set_kernel_timing(ctx.h, 0), "pbg_set_kernel_timing")
     ctx.close()

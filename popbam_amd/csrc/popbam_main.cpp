@@ -803,6 +803,7 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
             const int pr = pbg_stream_push(st, &pl);
             const auto tf = Clock::now();
             freer()->put(p);
+            p = pbf_keys{};   // owned by the freer now: EarlyFree must not free it again on a throw
             prof.add("push_calls_s", secs(tp, tf));
             prof.add("keys_free_s", secs(tf, Clock::now()));
             if (pr != PBG_OK) throw Fatal{std::string("pbg_stream_push failed: ") + pbg_last_error(ctx)};

@@ -17,6 +17,8 @@ def _parse(argv, monkeypatch):
     (["--config", "3"], 1 << 27, 24),
     (["--config", "3", "--overlap"], 1 << 25, 24),
     (["--config", "3", "--chunk", str(1 << 26)], 1 << 26, 24),
+    (["--config", "3", "--chunk", str(1 << 25)], 1 << 25, 24),   # explicit 2^25 kept (was the argparse default)
+    (["--config", "4", "--chunk", str(1 << 25)], 1 << 25, 96),
     (["--config", "4"], 1 << 23, 96),
 ])
 def test_config_defaults(monkeypatch, argv, chunk, samples):
