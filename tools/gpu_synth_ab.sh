@@ -1,5 +1,5 @@
 #!/bin/bash
-# Generator A/B: tools/synth_bench.py (configs[3] chunk shape by default) under a kernel trace for
+# Generator A/B: tools/synth_bench.py --allow-variant (configs[3] chunk shape by default) under a kernel trace for
 # the product library and each variant named (popbam_amd/variants/NAME).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; O=gpurun_out/synth_ab; mkdir -p $O; export TMPDIR=/tmp
