@@ -73,6 +73,25 @@ def pmc_traffic(config: int, shape: dict) -> dict | None:
     return d
 
 
+HBM_ACHIEVABLE_GBS = 6290.0   # measured float4-copy rate (MI355X_MICROARCH.md), the most HBM delivers
+
+
+def traffic_split(traffic: int | None, ms: float) -> dict | None:
+    """What a counted `traffic` (FETCH_SIZE x 2 + WRITE_SIZE, bytes per launch) can mean at the
+    launch's duration.  FETCH_SIZE counts the L2's fabric requests, Infinity-Cache (MALL) hits
+    included (MI355X_MICROARCH.md, HBM / rocprofv3 section), so the count is an upper bound of the
+    HBM bytes: at most HBM_ACHIEVABLE_GBS x duration of it can have come from HBM, the rest was served
+    by the Infinity Cache.  A ratio above 1 over the algorithmic bytes is then not all HBM waste."""
+    if not traffic or ms <= 0:
+        return None
+    cap = HBM_ACHIEVABLE_GBS * 1e9 * ms * 1e-3
+    return {"counted_GBps": round(traffic / (ms * 1e-3) / 1e9, 1), "hbm_achievable_GBps": HBM_ACHIEVABLE_GBS,
+            "hbm_bytes_at_most": int(min(traffic, cap)), "infinity_cache_bytes_at_least": int(max(0.0, traffic - cap)),
+            "note": "traffic = L2 fabric requests (FETCH_SIZE x 2 + WRITE_SIZE), Infinity-Cache hits included; "
+                    "at this launch's duration HBM can deliver at most hbm_bytes_at_most of it (6.29 TB/s "
+                    "achievable), the rest came from the 256 MiB Infinity Cache"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -713,6 +732,7 @@ def bench_genome(args, torch, dist, world, rank, binfo):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_pass / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "bytes_per_launch": bpl, "ms_per_launch": round(scan_ms, 4),
                          "traffic_ratio": round(traffic / bpl, 4) if traffic else None,
+                         "traffic_split": traffic_split(traffic, scan_ms),
                          "call_stage_traffic": call_traffic,
                          "traffic_source": (f"{pmc['file']} (src_sha {pmc['src_sha']}, {pmc['source']}; mean over the "
                                             f"pass's chunk launches)" if pmc else
@@ -988,6 +1008,7 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "bytes_per_launch": scan_bytes_launch, "ms_per_launch": round(scan_ms, 4),
                          "traffic_ratio": round(traffic / scan_bytes_launch, 4) if traffic else None,
+                         "traffic_split": traffic_split(traffic, scan_ms),
                          "traffic_source": (f"{pmc['file']} (src_sha {pmc['src_sha']}, {pmc['source']})" if pmc else
                                             "no PMC profile of this source tree (tools/pmc_traffic.sh)"),
                          "bytes_basis": "SURVEY 8(d): sum over (position, sample) of 2k+5, +1 +row_bytes per position",

@@ -366,6 +366,12 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         HIPCHK(c, hipMalloc((void **)&c->deep.raw, (size_t)nblk * blk_cap * 3 * sizeof(uint4)));
         c->deep_sites_cap = pl->n_sites;
         c->deep_info_cap = ntask;
+        // allocated lengths, for the PBG_BOUNDS store checks
+        c->deep.raw_n = c->deep.raw_chk = (uint64_t)nblk * blk_cap * 3;
+        c->deep.info_n = c->deep.info_chk = ntask;
+        c->deep.tasks_n = c->deep.tasks_chk = c->deep.task_cap;
+        c->deep.blk_n = c->deep.blk_chk = nblk;
+        c->deep.sites_n = c->deep.sites_chk = pl->n_sites;
     }
     if (!c->deep.count) HIPCHK(c, hipMalloc((void **)&c->deep.count, 4 * sizeof(uint32_t)));
     hipEvent_t e0 = nullptr, e1 = nullptr, c0 = nullptr, c1 = nullptr;
@@ -387,11 +393,26 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         HIPCHK(c, hipEventRecord(c0, (hipStream_t)stream));
     }
     uint32_t shrink = 0;
+    pbg::DeepBufs D = c->deep;
+    D.rows_div = D.words_div = 1;
 #ifdef PBG_BOUNDS
-    if (const char *st = std::getenv("PBG_BOUNDS_SELFTEST")) shrink = std::atoi(st) > 0 ? 8u : 0u;
+    // positive controls of the bounds build: PBG_BOUNDS_SELFTEST names the class whose checked
+    // range is cut (keys: the batch's last chunk; queue / info / block: half the array; deep: all
+    // of it; rows / words: half the batch; pool: pbg_window_stats), so correct kernels trip that
+    // class's check
+    if (const char *st = std::getenv("PBG_BOUNDS_SELFTEST")) {
+        const std::string m = st;
+        if (m == "1" || m == "keys") shrink = 8u;
+        else if (m == "queue") D.raw_chk = D.raw_n / 2;
+        else if (m == "info") D.info_chk = D.info_n / 2;
+        else if (m == "deep") D.tasks_chk = 0;
+        else if (m == "block") D.blk_chk = D.blk_n / 2;
+        else if (m == "rows") D.rows_div = 2;
+        else if (m == "words") D.words_div = 2;
+    }
 #endif
     const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys, c->d_err, c->scan_masked, shrink};
-    HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, B, cap, rows, cb, c->d_err, c->deep,
+    HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, B, cap, rows, cb, c->d_err, D,
                                      (hipStream_t)stream, e0, e1, c->n_cu));
     if (c1) HIPCHK(c, hipEventRecord(c1, (hipStream_t)stream));
     return PBG_OK;
@@ -412,6 +433,13 @@ int pbg_check(pbg_ctx *c, void *stream) {
     HIPCHK(c, hipMemset(c->d_err, 0, sizeof(int)));
     if (herr & 4) return fail(c, PBG_E_RANGE, "statistics workspace exhausted (windows with very many segregating sites)");
     if (herr & 8) return fail(c, PBG_E_BATCH, "a kernel loaded keys outside [block_off[0], block_off[last]) (PBG_BOUNDS build)");
+    if (herr & pbg::kErrQueue) return fail(c, PBG_E_BATCH, "a queue record was stored outside its block's region of the queue (PBG_BOUNDS build)");
+    if (herr & pbg::kErrDeep) return fail(c, PBG_E_BATCH, "a deep-task entry was stored outside the task list (PBG_BOUNDS build)");
+    if (herr & pbg::kErrInfo) return fail(c, PBG_E_BATCH, "an info byte was stored outside the info array (PBG_BOUNDS build)");
+    if (herr & pbg::kErrRow) return fail(c, PBG_E_BATCH, "a row was stored outside the batch's rows (PBG_BOUNDS build)");
+    if (herr & pbg::kErrBlock) return fail(c, PBG_E_BATCH, "a block's pending mask / queue count / overflow entry was stored out of range (PBG_BOUNDS build)");
+    if (herr & pbg::kErrWords) return fail(c, PBG_E_BATCH, "a consensus word was stored outside the batch's words (PBG_BOUNDS build)");
+    if (herr & pbg::kErrPool) return fail(c, PBG_E_BATCH, "a statistics workspace store fell outside its pool slice (PBG_BOUNDS build)");
     if (herr & 2) return fail(c, PBG_E_BATCH, "synthetic batch needs more keys than keys_cap");
     return fail(c, PBG_E_BATCH, "pileup block_off disagrees with k[]");
 }
@@ -464,6 +492,11 @@ int pbg_window_stats(pbg_ctx *c, const void *rows, uint32_t n_rows, const pbg_wi
     }
     HIPCHK(c, hipSetDevice(c->device));
     pbg::StatsArgs A{};
+    A.pool_div = 1;
+#ifdef PBG_BOUNDS
+    if (const char *st = std::getenv("PBG_BOUNDS_SELFTEST"))
+        if (std::string(st) == "pool") A.pool_div = 2;   // positive control of the pool store checks
+#endif
     A.stats = o->stats;
     A.min_freq = o->min_freq;
     A.outidx = o->outidx;

@@ -291,7 +291,11 @@ struct StatsArgs {
     int32_t *ld_ns;                       // [n_win*npops] ZnS: the reference's num_snps
     pbg_window_out out;
     WinLds lds;
+    // PBG_BOUNDS store checks: pool / ZnS-list stores must fall in the first len / pool_div
+    // words of the slice they belong to (1; 2 in the PBG_BOUNDS_SELFTEST=pool positive control)
+    uint32_t pool_div;
 };
+#define PBG_POOL_OK(A, idx, lo, len) PBG_STORE_OK((A).err, (idx) - (lo), (len) / (A).pool_div, len, ::pbg::kErrPool)
 
 // Samples deeper than the register sort width (16 reads) are finished outside the main call
 // kernel: it queues them as tasks (lane-per-task kernel), parks the position's other per-sample
@@ -318,6 +322,16 @@ struct DeepBufs {
     uint64_t *pend;     // rows-only pipeline: per block, the positions whose row waits for a queued task
     uint4 *raw;         // [nblk*blk_cap*3] 48-byte queue records {site, sample | k << 8, sum mapQ^2,
                         // reference byte} + the task's 16 keys (0 past k): all call_slow_kernel reads
+    // PBG_BOUNDS store checks (unused by the product build): each array's allocated length
+    // (elements) and the length the checks allow -- equal, except in a PBG_BOUNDS_SELFTEST mode,
+    // which halves one of them so correct kernels trip that class's check (api.cpp)
+    uint64_t raw_n, raw_chk;       // uint4 entries of raw
+    uint64_t info_n, info_chk;     // bytes of info
+    uint32_t tasks_n, tasks_chk;   // entries of tasks
+    uint32_t blk_n, blk_chk;       // entries of blk_cnt / pend
+    uint32_t sites_n, sites_chk;   // entries of sites
+    uint32_t rows_div;             // rows the checks allow = n_sites / rows_div (1; 2 in the rows self-test)
+    uint32_t words_div;            // consensus words allowed = n_sites * n / words_div
 };
 #ifndef PBG_QGROUP
 #define PBG_QGROUP 16
@@ -363,6 +377,37 @@ __device__ __forceinline__ void bounds_chunk(const Batch &B, uint64_t c) {   // 
 #define PBG_BOUNDS_KEYS(B, lo, n) ((void)0)
 #define PBG_BOUNDS_CHUNK(B, c) ((void)0)
 #endif
+
+// Store checks of the same build: every device store and bump of the call kernels names its
+// array's class and is checked against that array's allocation (DeepBufs::*_n / *_chk, the
+// batch's n_sites for rows; the statistics pool against its capacity).  An index at or past
+// the checked length sets the class's err bit (pbg_check reports which); an index past the real
+// allocation is also not stored, so a bounds build reports a wild store instead of faulting.
+// The product build compiles every guard to `true`.
+constexpr int kErrQueue = 16;    // call_scan_kernel's 48-byte queue records (D.raw, the block's region)
+constexpr int kErrDeep = 32;     // deep-task list entries (D.tasks)
+constexpr int kErrInfo = 64;     // per-(position, sample) info bytes (D.info)
+constexpr int kErrRow = 128;     // packed rows
+constexpr int kErrBlock = 256;   // per-block bookkeeping: D.pend, D.blk_cnt, D.sites
+constexpr int kErrWords = 512;   // consensus words (cb_out)
+constexpr int kErrPool = 1024;   // statistics workspace (pool / ZnS lists)
+#ifdef PBG_BOUNDS
+__device__ __forceinline__ bool store_guard(int *err, uint64_t idx, uint64_t chk, uint64_t lim, int bit) {
+    if (idx >= chk) atomicOr(err, bit);
+    return idx < lim;
+}
+#define PBG_STORE_OK(err, idx, chk, lim, bit) \
+    ::pbg::store_guard((err), (uint64_t)(idx), (uint64_t)(chk), (uint64_t)(lim), (bit))
+#else
+#define PBG_STORE_OK(err, idx, chk, lim, bit) true
+#endif
+// the classes' guards (D: DeepBufs, n_sites: the batch's positions = its rows)
+#define PBG_ROW_OK(err, D, n_sites, s) PBG_STORE_OK(err, s, (n_sites) / (D).rows_div, n_sites, ::pbg::kErrRow)
+#define PBG_INFO_OK(err, D, i) PBG_STORE_OK(err, i, (D).info_chk, (D).info_n, ::pbg::kErrInfo)
+#define PBG_BLK_OK(err, D, b) PBG_STORE_OK(err, b, (D).blk_chk, (D).blk_n, ::pbg::kErrBlock)
+#define PBG_SITES_OK(err, D, i) PBG_STORE_OK(err, i, (D).sites_chk, (D).sites_n, ::pbg::kErrBlock)
+#define PBG_TASK_OK(err, D, i) PBG_STORE_OK(err, i, (D).tasks_chk, (D).tasks_n, ::pbg::kErrDeep)
+#define PBG_WORD_OK(err, D, n_words, i) PBG_STORE_OK(err, i, (n_words) / (D).words_div, n_words, ::pbg::kErrWords)
 
 // kernel launchers (defined in call_kernel.hip / stats_kernel.hip)
 // n_cu: the context device's CU count (sizes the persistent queue kernel's grid).

@@ -797,10 +797,17 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
         prof.add("stream_open_s", secs(t0, Clock::now()));
         t0 = Clock::now();
         bool first = true;
+        // POPBAM_FAULT_PUSH=k (tests only): the k-th push of the run reports a failure, so the error
+        // path -- pieces already handed to the freer, the rest still owned here -- is exercised
+        const long fault_at = env_int("POPBAM_FAULT_PUSH", 0);
+        long pushes = 0;
+        auto push = [&](const pbg_pileup &pl) {
+            return ++pushes == fault_at ? PBG_E_BATCH : pbg_stream_push(st, &pl);
+        };
         for (pbf_keys &p : early) {
             const auto tp = Clock::now();
             pbg_pileup pl{p.n_sites, p.pos0, p.ref, p.k, p.rmsq, p.block_off, p.keys};
-            const int pr = pbg_stream_push(st, &pl);
+            const int pr = push(pl);
             const auto tf = Clock::now();
             freer()->put(p);
             p = pbf_keys{};   // owned by the freer now: EarlyFree must not free it again on a throw
@@ -824,7 +831,7 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
                 break;
             }
             pbg_pileup pl{p.n_sites, p.pos0, p.ref, p.k, p.rmsq, p.block_off, p.keys};
-            const int pr = pbg_stream_push(st, &pl);
+            const int pr = push(pl);
             freer()->put(p);
             if (pr != PBG_OK) throw Fatal{std::string("pbg_stream_push failed: ") + pbg_last_error(ctx)};
         }

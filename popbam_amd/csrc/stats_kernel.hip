@@ -198,7 +198,15 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
 #define PBG_WIN_AHEAD 4
 #endif
     constexpr int kLoadAhead = PBG_WIN_AHEAD;
+    // PBG_BOUNDS: a pool store at word idx must lie in the slice [sl_lo, sl_lo + sl_len) the
+    // window took (compact's second pass writes there; its first pass writes LDS)
+    uint64_t sl_lo = 0, sl_len = 0;
+    auto pool_ok = [&](uint64_t idx) { return PBG_POOL_OK(A, idx, sl_lo, sl_len); };
+    (void)pool_ok;
+    (void)sl_len;
     auto compact = [&](M *dst, uint32_t cap, bool count_sites, int &my_counted) -> uint32_t {
+        const bool in_pool = dst != s_seg;
+        (void)in_pool;
         uint32_t S = 0;
         uint4 qa[kLoadAhead];
         for (int64_t cg = c0; cg < c1; cg += 64 * kLoadAhead) {
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if ((segm >> r) & 1u) {
-                    if (j < cap) dst[j] = t[r];
+                    if (j < cap && (!in_pool || pool_ok(sl_lo + (uint64_t)j * NW))) dst[j] = t[r];
                     ++j;
                 }
             S += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -286,12 +294,15 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
         }
         wsg = reinterpret_cast<M *>(A.pool + off);
         wpl = A.pool + off + S * NW;
+        sl_lo = off;
+        sl_len = size;
         __syncthreads();
         if (over) {
             int unused = 0;
             (void)compact(wsg, S, false, unused);   // second pass, only for windows beyond segcap
         } else {
-            for (uint32_t j = (uint32_t)lane; j < S; j += 64) wsg[j] = s_seg[j];
+            for (uint32_t j = (uint32_t)lane; j < S; j += 64)
+                if (pool_ok(sl_lo + (uint64_t)j * NW)) wsg[j] = s_seg[j];
         }
     }
     __syncthreads();
@@ -318,7 +329,7 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                 if (v < plane_n) {
                     uint64_t m = 0;
                     for (uint32_t j = 0; j < S; ++j) m |= (uint64_t)bit(s_seg[j], v) << j;
-                    plane[v] = m;
+                    if (plane != wpl || pool_ok((uint64_t)(plane - A.pool) + (uint64_t)v)) plane[v] = m;
                 }
             }
         } else {
@@ -327,7 +338,8 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                 const M t = j < S ? seg_at(j) : M{};
                 for (int v = 0; v < plane_n; ++v) {
                     const uint64_t m = __ballot(bit(t, v));
-                    if (lane == 0) plane[v * nwords + k] = m;
+                    if (lane == 0 && (plane != wpl || pool_ok((uint64_t)(plane - A.pool) + (uint64_t)(v * nwords + k))))
+                        plane[v * nwords + k] = m;
                 }
             }
         }
@@ -512,7 +524,8 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                     if (j == S - 1) lastvar = v ? 1 : 0;
                 }
                 const uint64_t bm = __ballot(v);
-                if (v) vl[V + (uint32_t)__popcll(bm & ((1ULL << lane) - 1))] = t;
+                const uint32_t vi = V + (uint32_t)__popcll(bm & ((1ULL << lane) - 1));
+                if (v && PBG_POOL_OK(A, off + (uint64_t)vi * NW, off, zreg)) vl[vi] = t;
                 V += (uint32_t)__popcll(bm);
             }
             // num_snps: variable sites among the first S-1, plus the final increment
@@ -583,7 +596,8 @@ __global__ __launch_bounds__(64) void window_stats_kernel(DevParams P, DevTables
                     v = m >= mf && m <= nn - mf;
                 }
                 const uint64_t bm = __ballot(v);
-                if (v) vl[V + (uint32_t)__popcll(bm & ((1ULL << lane) - 1))] = t;
+                const uint32_t vi = V + (uint32_t)__popcll(bm & ((1ULL << lane) - 1));
+                if (v && PBG_POOL_OK(A, off + (uint64_t)vi * NW, off, (uint64_t)Vi * NW)) vl[vi] = t;
                 V += (uint32_t)__popcll(bm);
             }
             off += Vi * NW;
@@ -754,7 +768,10 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
                 M *u = uniq + (uint64_t)j * (uint64_t)S;
                 if (nonzero(type) && type < pm) {
                     if (ns[j] == 0) {
-                        u[nu[j]++] = type;
+                        if (PBG_POOL_OK(A, A.win_off[2 * w + 1] + ((uint64_t)j * S + nu[j]) * NW, A.win_off[2 * w + 1],
+                                        (uint64_t)np * S * NW))
+                            u[nu[j]] = type;
+                        ++nu[j];
                         last_type = type;
                         ns[j]++;
                     } else {
@@ -763,7 +780,10 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
                             bool seen = false;
                             for (int q = 0; q < nu[j]; q++) seen |= (u[q] == type) || (u[q] == comp);
                             if (!seen) {
-                                u[nu[j]++] = type;
+                                if (PBG_POOL_OK(A, A.win_off[2 * w + 1] + ((uint64_t)j * S + nu[j]) * NW,
+                                                A.win_off[2 * w + 1], (uint64_t)np * S * NW))
+                                    u[nu[j]] = type;
+                                ++nu[j];
                                 part[j]++;
                             }
                         }
@@ -804,7 +824,10 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
                 const M t = seg[j] & pm;
                 if (variable(pc(t))) {
                     if (j < S - 1) ++ns;
-                    vt[V++] = t;
+                    if (PBG_POOL_OK(A, A.win_off[2 * w + 1] + ((uint64_t)i * S + V) * NW, A.win_off[2 * w + 1],
+                                    (uint64_t)np * S * NW))
+                        vt[V] = t;
+                    ++V;
                 }
             }
             ++ns;

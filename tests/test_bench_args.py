@@ -27,3 +27,17 @@ def test_config_defaults(monkeypatch, argv, chunk, samples):
     assert a.chunk % 64 == 0   # whole 64-position blocks (genome.GenomePass)
     if a.config == 3 and len(argv) == 2:
         assert a.chunk >= a.contig_len   # the default serial pass: one chunk per contig
+
+
+def test_traffic_split_bounds_the_hbm_share():
+    """A counted traffic above what HBM can deliver in the launch's time is labelled as at least
+    that excess served by the Infinity Cache (configs[3]'s 104.7 GB in 15.385 ms
+    is 6.81 TB/s counted, above the 6.29 TB/s achievable)."""
+    import bench
+    s = bench.traffic_split(104_700_000_000, 15.385)
+    assert s["counted_GBps"] > bench.HBM_ACHIEVABLE_GBS
+    assert s["hbm_bytes_at_most"] == int(6290e9 * 15.385e-3)
+    assert s["hbm_bytes_at_most"] + s["infinity_cache_bytes_at_least"] == 104_700_000_000
+    s = bench.traffic_split(20_370_000_000, 3.4142)   # configs[2]: within what HBM can deliver
+    assert s["infinity_cache_bytes_at_least"] == 0
+    assert bench.traffic_split(None, 3.0) is None

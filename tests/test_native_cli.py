@@ -161,3 +161,22 @@ def test_native_profile_phases(gpu_lib, tmp_path):
     for k in ("parse_s", "fasta_s", "hip_init_s", "pbg_create_s", "walk_push_s", "finish_s", "run_s"):
         assert k in p and p[k] >= 0, k
     assert p["blocks"] == 1 and p["gpu"]["chunks"] >= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault_at", [1, 2, 5, 40])
+def test_native_push_failure_exits_cleanly(gpu_lib, fault_at):
+    """A failing pbg_stream_push (POPBAM_FAULT_PUSH=k: the k-th push of the run reports an error)
+    ends the process like fatal_error -- the message, "Exiting program", status 1 -- whether the
+    failing piece was one taken while the GPU context was built (the others then still owned by
+    the run) or one of the walk's later pieces: no double free, no abort."""
+    name = "g01_base"
+    cs = fixtures.load_case(name)["meta"]["cases"][0]
+    rc, out, err = _run(_argv(name, cs), env={"POPBAM_FAULT_PUSH": str(fault_at), "POPBAM_FEED_CHUNK": "64",
+                                              "POPBAM_FEED_THREADS": "3"})
+    if rc == 0:   # fewer pushes than fault_at: the run is the reference's
+        assert fault_at > 2, err
+        return
+    assert rc == 1, (rc, err)
+    assert "popbam runtime error:" in err and "pbg_stream_push failed" in err and "Exiting program" in err
+    assert out == ""
