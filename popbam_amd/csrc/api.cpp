@@ -215,6 +215,32 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
         for (int nn = 0; nn <= 16; ++nn)
             for (int kk = 0; kk <= 16; ++kk) oe[60 * 17 + nn * 17 + kk] = lhet[nn << 8 | kk];
         if ((e = upload(&c->d_oe, oe)) != hipSuccess) return bad(e, "upload one-error tables");
+        {   // call_scan_kernel's LDS image of the same tables (pbg_common.h ScanTab)
+            pbg::ScanTab st{};
+            for (int q = 4; q < 64; ++q)
+                for (int dd = 3; dd <= 16; ++dd) {
+                    const volatile double pe = fk[0] * beta[q << 16 | dd << 8];   // one_error_ref's product
+                    st.fpe[(q - 4) * 14 + dd - 3] = (float)pe;
+                }
+            for (int lev = 0; lev < 15; ++lev)
+                for (int dd = 3; dd <= 16; ++dd) {
+                    const double b = lb[17 + (4 * lev) * 17 + dd];   // q = 4 + 4 lev: a bound for the level
+                    float f = (float)b;
+                    if ((double)f > b) f = std::nextafter(f, 0.0f);   // rounded down
+                    st.lq[lev * 14 + dd - 3] = f;
+                }
+            for (int dd = 3; dd <= 16; ++dd) {
+                const int idx[4][2] = {{dd, dd - 1}, {dd, 1}, {dd - 1, 0}, {dd - 1, dd - 1}};
+                for (int i = 0; i < 4; ++i) {
+                    const volatile double h = -4.343 * lhet[idx[i][0] << 8 | idx[i][1]];
+                    st.lh[(dd - 3) * 4 + i] = h;
+                }
+            }
+            for (int m = 0; m <= 16; ++m) st.pre[m] = lb[m];
+            if ((e = hipMalloc(&c->d_scantab, sizeof(st))) != hipSuccess) return bad(e, "hipMalloc scan tables");
+            if ((e = hipMemcpy(c->d_scantab, &st, sizeof(st), hipMemcpyHostToDevice)) != hipSuccess)
+                return bad(e, "upload scan tables");
+        }
         std::vector<double> bu(60 * 17, 0.0);   // min over q' >= q, c <= d - 1 of beta[q'][d][c]
         for (int dd = 1; dd <= 16; ++dd) {
             double run = 1e300;
@@ -274,6 +300,7 @@ int pbg_create(pbg_ctx **out, int device, const pbg_params *p) {
     c->dt.fbeta = c->d_fbeta;
     c->dt.lb = c->d_lb;
     c->dt.oe = c->d_oe;
+    c->dt.scantab = reinterpret_cast<const uint4 *>(c->d_scantab);
     c->dt.a1 = c->d_sfs;
     c->dt.a2 = c->d_sfs + L;
     c->dt.e1 = c->d_sfs + 2 * L;
@@ -288,7 +315,7 @@ void pbg_destroy(pbg_ctx *c) {
     (void)hipSetDevice(c->device);
     pbg::stream_bufs_free(c);
     for (void *p : {(void *)c->d_fk, (void *)c->d_beta, (void *)c->d_lhet, (void *)c->d_sfs, (void *)c->d_r2,
-                    (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_oe, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, (void *)c->d_zns,
+                    (void *)c->d_fbeta, (void *)c->d_lb, (void *)c->d_oe, c->d_scantab, (void *)c->d_err, (void *)c->d_ws, (void *)c->d_wsoff, (void *)c->d_zns,
                     (void *)c->deep.sites, (void *)c->deep.tasks, (void *)c->deep.info, (void *)c->deep.count,
                     (void *)c->deep.blk_cnt, (void *)c->deep.raw, (void *)c->deep.pend,
                     (void *)c->d_segcnt, (void *)c->d_synth})

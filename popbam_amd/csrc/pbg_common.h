@@ -85,12 +85,27 @@ struct DevTables {
     // [0, 60 * 17) beta[q<<16|d<<8|0] at (q - 4) * 17 + d; then [60 * 17, 60 * 17 + 17 * 17)
     // lhet[n<<8|k] at 60 * 17 + n * 17 + k (n, k <= 16)
     const double *oe;     // [kOeSize]
+    // call_scan_kernel's one-error tables as one image its workgroups copy to LDS (ScanTab, n <= 12):
+    // fpe[(q - 4) * 14 + d - 3] = (float)(fk[0] * beta[q<<16|d<<8|0]) (the one double multiply and
+    // narrowing one_error_ref does); lq[((q - 4) >> 2) * 14 + d - 3] = lb[17 + (q - 4) * 17 + d] at the
+    // level's lowest q, rounded down to float (a lower bound of the bound: the test stays exact,
+    // a few more tasks queue); lh[(d - 3) * 4 + i] = -4.343 * lhet of {[d][d-1], [d][1], [d-1][0],
+    // [d-1][d-1]} (the double products one_error_ref forms); pre[m] = lb[m] (fk prefix sums)
+    const uint4 *scantab;
     const double *a1, *a2, *e1, *e2;          // Tajima/Fay-Wu constants (pop_sfs.cpp:511-571)
     const double *r2;     // concatenated per-population r^2 tables, see r2_off
     int32_t r2_off[PBG_MAX_POPS];             // offset of population p's (n_p+1)^3 table
 };
 
 constexpr int kLbSize = 17 + 60 * 17;
+struct ScanTab {
+    float fpe[60 * 14];
+    float lq[15 * 14];
+    double lh[14 * 4];
+    double pre[17];
+};
+static_assert(sizeof(ScanTab) % 16 == 0, "ScanTab is copied as uint4");
+constexpr int kScanTabVec = (int)(sizeof(ScanTab) / 16);
 constexpr int kOeSize = 60 * 17 + 17 * 17;
 constexpr int kFbetaN = 17;   // n in [0, 16]
 __host__ __device__ inline uint32_t fbeta_index(uint32_t q, uint32_t n, uint32_t c, uint32_t w) {

@@ -63,6 +63,7 @@ struct pbg_ctx {
     double *d_fbeta = nullptr;
     double *d_lb = nullptr;
     double *d_oe = nullptr;
+    void *d_scantab = nullptr;   // pbg::ScanTab (call_scan_kernel's LDS image)
     int *d_err = nullptr;
     int scan_masked = 0;   // the next pbg_call_sites' Batch::masked (set by pbg_stream_push from the host reference)
     std::string err;
