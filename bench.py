@@ -386,8 +386,10 @@ def end_to_end(args, torch, ctx, hp, wins) -> dict:
         _, texts, prof = run()
     dt = (time.perf_counter() - t0) / passes
     same = same and texts == want
+    compact = end_to_end_compact(args, torch, ctx, hp, cmds, want, host)
     del host
     return {"Msites_per_s": round(args.sites / dt / 1e6, 2), "ms_per_run": round(dt * 1e3, 2),
+            "Msites_per_s_compact": compact["Msites_per_s"], "compact": compact,
             "h2d_bytes_per_run": prof["h2d_bytes"], "h2d_GBps_effective": round(prof["h2d_bytes"] / dt / 1e9, 2),
             "chunks": prof["chunks"], "pinned_chunks": prof["pinned_chunks"],
             "ms_h2d_device": round(prof["ms_h2d"], 2), "ms_call_device": round(prof["ms_call"], 2),
@@ -395,6 +397,63 @@ def end_to_end(args, torch, ctx, hp, wins) -> dict:
             "how": "C-ABI pbg_stream_*: pinned host key batch (SURVEY 8(d) layout) -> H2D chunks on a copy stream "
                    "into two device slots, pbg_call_sites per chunk on the compute stream, then nucdiv + sfs + ld "
                    "over all windows and their TSV; wall time per run (open -> three texts)"}
+
+
+def end_to_end_compact(args, torch, ctx, hp, cmds, want, host) -> dict:
+    """The same streamed run with COMPACT pieces (pbg_stream_push_compact): the reference-only
+    tasks' keys stay on the host (rmsq bit 31 flags them; the feeder flags them as it packs, here
+    pbf_compact converts the pinned host batch once, before timing), so far fewer bytes cross
+    PCIe.  Rows and texts must equal the resident step's."""
+    import numpy as np
+    from popbam_amd import _lib, feed
+    n = ctx.params.n_samples
+    full = {k: host[k].numpy() for k in ("ref", "k", "rmsq", "keys", "block_off")}
+    full["k"] = full["k"].reshape(args.sites, n)
+    full["rmsq"] = full["rmsq"].reshape(args.sites, n)
+    t0 = time.perf_counter()
+    c = feed.compact(full, n, ctx.k_bytes)
+    t_conv = time.perf_counter() - t0
+    signed = {np.dtype(np.uint16): np.int16, np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+    pin = {}
+    for k, v in c.items():
+        if k == "pos0":
+            continue
+        a = np.ascontiguousarray(v).reshape(-1)
+        pin[k] = torch.from_numpy(a.view(signed.get(a.dtype, a.dtype))).pin_memory()
+    del c, full
+    piece = _lib.PbgPileup(args.sites, 0, pin["ref"].data_ptr(), pin["k"].data_ptr(), pin["rmsq"].data_ptr(),
+                           pin["block_off"].data_ptr(), pin["keys"].data_ptr())
+
+    def run():
+        with _lib.Stream(ctx, cmds, 0, args.sites, args.e2e_chunk) as st:
+            st.push(piece, compact=True)
+            st.finish()
+            return st, [st.text(i) for i in range(len(cmds))], st.profile()
+
+    rows = torch.empty_like(hp.rows)
+    with _lib.Stream(ctx, cmds, 0, args.sites, args.e2e_chunk) as st:   # warmup
+        st.push(piece, compact=True)
+        st.finish()
+        st.rows_into(rows.data_ptr(), rows.numel())
+        texts = [st.text(i) for i in range(len(cmds))]
+    torch.cuda.synchronize()
+    same = bool(torch.equal(rows, hp.rows)) and texts == want
+    passes = max(1, args.e2e_passes)
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        _, texts, prof = run()
+    dt = (time.perf_counter() - t0) / passes
+    same = same and texts == want
+    keys_kept = int(pin["keys"].numel())
+    del pin
+    return {"Msites_per_s": round(args.sites / dt / 1e6, 2), "ms_per_run": round(dt * 1e3, 2),
+            "h2d_bytes_per_run": prof["h2d_bytes"], "h2d_GBps_effective": round(prof["h2d_bytes"] / dt / 1e9, 2),
+            "keys_in_piece": keys_kept, "chunks": prof["chunks"], "ms_h2d_device": round(prof["ms_h2d"], 2),
+            "ms_call_device": round(prof["ms_call"], 2), "ms_finish": round(prof["ms_finish"], 2),
+            "host_conversion_s": round(t_conv, 2), "runs": passes, "matches_resident": same,
+            "how": "C-ABI pbg_stream_push_compact: reference-only tasks flagged in rmsq bit 31 without their keys "
+                   "(pbf_compact of the pinned host batch, untimed: the feeder emits this form as it packs), then "
+                   "the streamed run as above"}
 
 
 def cli_rate(args) -> dict:

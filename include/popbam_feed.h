@@ -65,6 +65,10 @@ typedef struct {
     int32_t min_baseQ, min_mapQ;   /* -b / -a as the reference holds them (unsigned char)     */
     int32_t illumina;              /* BAM_ILLUMINA (-i): baseQ > 31 ? baseQ - 31 : 0          */
     int32_t k_bytes;               /* width of k[]: 1 (max_depth <= 255) or 2 (pbg_k_bytes)   */
+    int32_t compact;               /* pieces in the compact form of pbg_stream_push_compact: a
+                                      reference-only task (1..32 keys, all on the upper-case
+                                      A/C/G/T reference base of a called position) gets rmsq bit
+                                      31 and no keys (needs max_depth <= 33025)                */
 } pbf_filter;
 
 const char *pbf_last_error(void);   /* thread-local */
@@ -106,6 +110,9 @@ int  pbf_pileup_mt(const char *bam_path, int n_threads, int32_t chunk, int tid, 
  * in pileup order.  Arrays allocated by the library; release with pbf_keys_free.          */
 int  pbf_pack(const pbf_batch *raw, int n_samples, const pbf_filter *f, pbf_keys *out);
 void pbf_keys_free(pbf_keys *keys);
+/* A full key batch (pbf_keys / pbg_pileup layout) in the compact form (pbf_filter.compact):
+ * allocated by the library, release with pbf_keys_free.  k_bytes: width of in->k.          */
+int  pbf_compact(const pbf_keys *in, int n_samples, int k_bytes, pbf_keys *out);
 
 /* pbf_pileup_mt + pbf_pack, through the piece stream below (pbf_kstream_*) merged into one
  * batch: the raw reads of the whole region are never held at once.  Same batch as

@@ -277,6 +277,18 @@ typedef struct {
 int  pbg_stream_open(pbg_ctx *ctx, const pbg_cmd *cmds, uint32_t n_cmd, int32_t pos0, uint32_t n_sites,
                      uint32_t chunk_sites, pbg_stream **st);
 int  pbg_stream_push(pbg_stream *st, const pbg_pileup *host_piece);
+/* The same for a COMPACT piece (rows-only streams: not snp -o 0; max_depth <= 33025): a task
+ * (position, sample) whose rmsq[] has bit 31 set is reference-only -- the position is called back
+ * (ref bit 7 clear), its reference byte is an upper-case A/C/G/T, it has 1..32 keys and every key
+ * shows that base -- and its keys are left out of keys[]: block_off counts the keys present, k[]
+ * keeps the task's key count and rmsq[] bits 0..30 its sum of mapQ^2 (qfilter).  The scan settles
+ * such a task from k and rmsq alone (it does the same for the full piece's reference-only tasks),
+ * so the rows equal the full piece's; the other tasks are exactly as in pbg_stream_push.  About
+ * 92 % of the keys of a depth-10 panel belong to reference-only tasks, so the piece crosses PCIe
+ * in about a quarter of the bytes.  A flag on a task that cannot be reference-only is reported by
+ * pbg_stream_finish (PBG_E_BATCH).  Replaces nothing in the reference: call_base's per-read loop
+ * (popbam.cpp:266-287) already walks every key of the task, where the test costs a compare. */
+int  pbg_stream_push_compact(pbg_stream *st, const pbg_pileup *host_piece);
 int  pbg_stream_finish(pbg_stream *st);   /* waits, checks (PBG_E_BATCH ...), prints every command */
 /* command i's text (NUL-terminated); returns its length or PBG_E_RANGE with *needed set       */
 long pbg_stream_text(pbg_stream *st, uint32_t i, char *out, size_t cap, size_t *needed);

@@ -28,7 +28,7 @@ PBG_S_TREE = 0x400
 EXPORTS = ["pbg_create", "pbg_destroy", "pbg_last_error", "pbg_row_bytes", "pbg_k_bytes", "pbg_sfs_stride",
            "pbg_device_count", "pbg_call_sites", "pbg_window_stats", "pbg_check", "pbg_run", "pbg_take_text",
            "pbg_format", "pbg_build_info", "pbg_set_kernel_timing", "pbg_kernel_time", "pbg_call_time", "pbg_synth_max_keys",
-           "pbg_synth_pileup", "pbg_stream_open", "pbg_stream_push", "pbg_stream_finish", "pbg_stream_text",
+           "pbg_synth_pileup", "pbg_stream_open", "pbg_stream_push", "pbg_stream_push_compact", "pbg_stream_finish", "pbg_stream_text",
            "pbg_stream_rows", "pbg_stream_profile", "pbg_stream_error", "pbg_stream_close"]
 
 
@@ -156,6 +156,8 @@ def load(torch_first: bool = True):
     lib.pbg_stream_open.restype = C.c_int
     lib.pbg_stream_push.argtypes = [vp, P(PbgPileup)]
     lib.pbg_stream_push.restype = C.c_int
+    lib.pbg_stream_push_compact.argtypes = [vp, P(PbgPileup)]
+    lib.pbg_stream_push_compact.restype = C.c_int
     lib.pbg_stream_finish.argtypes = [vp]
     lib.pbg_stream_finish.restype = C.c_int
     lib.pbg_stream_text.argtypes = [vp, C.c_uint32, C.c_char_p, C.c_size_t, P(C.c_size_t)]
@@ -232,8 +234,13 @@ class Stream:
         ctx.check(ctx.lib.pbg_stream_open(ctx.h, arr, len(self.cmds), pos0, n_sites, chunk_sites, C.byref(self.h)),
                   "pbg_stream_open")
 
-    def push(self, piece: PbgPileup):
-        self.ctx.check(self.ctx.lib.pbg_stream_push(self.h, C.byref(piece)), "pbg_stream_push")
+    def push(self, piece: PbgPileup, compact: bool = False):
+        """pbg_stream_push, or pbg_stream_push_compact for a compact piece (rmsq bit 31 flags the
+        reference-only tasks whose keys the piece leaves out)."""
+        if compact:
+            self.ctx.check(self.ctx.lib.pbg_stream_push_compact(self.h, C.byref(piece)), "pbg_stream_push_compact")
+        else:
+            self.ctx.check(self.ctx.lib.pbg_stream_push(self.h, C.byref(piece)), "pbg_stream_push")
 
     def finish(self):
         self.ctx.check(self.ctx.lib.pbg_stream_finish(self.h), "pbg_stream_finish")

@@ -438,7 +438,9 @@ int pbg_call_sites(pbg_ctx *c, const pbg_pileup *pl, void *rows, uint64_t *cb, v
         else if (m == "words") D.words_div = 2;
     }
 #endif
-    const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys, c->d_err, c->scan_masked, shrink};
+    if (cb && c->scan_compact) return fail(c, PBG_E_ARG, "compact pieces carry no keys for reference-only tasks: no consensus words");
+    const pbg::Batch B{pl->n_sites, pl->ref, pl->k, pl->rmsq, pl->block_off, pl->keys, c->d_err, c->scan_masked, c->scan_compact,
+                       shrink};
     HIPCHK(c, pbg::launch_call_sites(c->row_bytes, c->dp, c->dt, B, cap, rows, cb, c->d_err, D,
                                      (hipStream_t)stream, e0, e1, c->n_cu));
     if (c1) HIPCHK(c, hipEventRecord(c1, (hipStream_t)stream));
@@ -466,6 +468,7 @@ int pbg_check(pbg_ctx *c, void *stream) {
     if (herr & pbg::kErrRow) return fail(c, PBG_E_BATCH, "a row was stored outside the batch's rows (PBG_BOUNDS build)");
     if (herr & pbg::kErrBlock) return fail(c, PBG_E_BATCH, "a block's pending mask / queue count / overflow entry was stored out of range (PBG_BOUNDS build)");
     if (herr & pbg::kErrWords) return fail(c, PBG_E_BATCH, "a consensus word was stored outside the batch's words (PBG_BOUNDS build)");
+    if (herr & pbg::kErrCompact) return fail(c, PBG_E_BATCH, "a compact piece flagged a task that is not reference-only (1..32 keys on an upper-case A/C/G/T reference base)");
     if (herr & pbg::kErrPool) return fail(c, PBG_E_BATCH, "a statistics workspace store fell outside its pool slice (PBG_BOUNDS build)");
     if (herr & 2) return fail(c, PBG_E_BATCH, "synthetic batch needs more keys than keys_cap");
     return fail(c, PBG_E_BATCH, "pileup block_off disagrees with k[]");

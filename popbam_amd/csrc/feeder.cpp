@@ -47,6 +47,18 @@ int fail(int code, const std::string &m) {
 using Clock = std::chrono::steady_clock;
 double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
+// Compact pieces (pbf_filter.compact, pbg_stream_push_compact): the scan's reference-only test
+// (call_kernel.hip call_scan_kernel) on the host -- 1..32 keys, every key's base (bits 0-1) the
+// base of an upper-case A/C/G/T reference byte at a called position (bit 7 clear).
+inline int ref_base_upper(uint8_t c) {
+    return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
+}
+inline bool all_on_base(const uint16_t *key, uint32_t n, uint32_t base) {
+    uint32_t x = 0;
+    for (uint32_t j = 0; j < n; ++j) x |= (key[j] & 3u) ^ base;
+    return x == 0;
+}
+
 // ---------------------------------------------------------------- raw deflate
 // BGZF blocks are raw deflate streams of at most 64 KB.  libdeflate (a system library of this
 // image, loaded at run time: its header is not installed) inflates a whole block in one call
@@ -1175,6 +1187,8 @@ int fast_walk(const RecSet &rs, int32_t cb, int32_t ce, const WalkCfg &cf, const
         }
         out->ref[i] &= 0x7F;   // a read spans pos: the pileup calls back here
         const size_t t0 = (size_t)i * ns;
+        // compact pieces: the reference base index of an upper-case A/C/G/T position, else -1
+        const int cmp_base = f.compact ? ref_base_upper(out->ref[i]) : -1;
         uint16_t *kd = keys.p + keys.n;
         size_t nk = 0;
         for (int s = 0; s < ns; ++s) {
@@ -1214,6 +1228,10 @@ int fast_walk(const RecSet &rs, int32_t cb, int32_t ce, const WalkCfg &cf, const
                 kout[t0 + s] = (uint8_t)kk;
             } else {
                 reinterpret_cast<uint16_t *>(kout)[t0 + s] = (uint16_t)kk;
+            }
+            if (cmp_base >= 0 && kk >= 1 && kk <= 32 && all_on_base(kd + nk - kk, kk, (uint32_t)cmp_base)) {
+                rq |= 0x80000000u;   // compact: reference-only, its keys left out
+                nk -= kk;
             }
             rout[t0 + s] = rq;
         }
@@ -1620,6 +1638,12 @@ int pbf_pack(const pbf_batch *raw, int ns, const pbf_filter *f, pbf_keys *out) {
         } else {
             ((uint16_t *)out->k)[t] = (uint16_t)kk;
         }
+        const uint8_t rc = raw->ref[t / ns];
+        const int cb = f->compact && !(rc & 0x80) ? ref_base_upper(rc) : -1;
+        if (cb >= 0 && kk >= 1 && kk <= 32 && all_on_base(out->keys + nk - kk, kk, (uint32_t)cb)) {
+            rq |= 0x80000000u;   // compact: reference-only, its keys left out
+            nk -= kk;
+        }
         out->rmsq[t] = rq;
     }
     if (r != raw->n_reads) {
@@ -1627,6 +1651,56 @@ int pbf_pack(const pbf_batch *raw, int ns, const pbf_filter *f, pbf_keys *out) {
         return fail(PBF_E_ARG, "depth[] does not add up to n_reads");
     }
     out->block_off[(L + 63) / 64] = nk;
+    out->n_keys = nk;
+    return PBF_OK;
+}
+
+int pbf_compact(const pbf_keys *in, int ns, int kb, pbf_keys *out) {
+    if (!in || !out || ns < 1 || (kb != 1 && kb != 2)) return fail(PBF_E_ARG, "bad argument");
+    memset(out, 0, sizeof(*out));
+    const uint32_t L = in->n_sites;
+    const size_t nt = (size_t)L * ns;
+    const uint32_t nblk = (L + 63) / 64;
+    out->n_sites = L;
+    out->pos0 = in->pos0;
+    out->ref = (uint8_t *)malloc(std::max<size_t>(L, 1));
+    out->k = malloc(std::max<size_t>(nt, 1) * kb);
+    out->rmsq = (uint32_t *)malloc(std::max<size_t>(nt, 1) * sizeof(uint32_t));
+    out->block_off = (uint64_t *)calloc(nblk + 2, sizeof(uint64_t));
+    const uint64_t k0 = in->block_off[0], ktot = in->block_off[nblk] - k0;
+    out->keys = (uint16_t *)aligned_alloc(16, (std::max<uint64_t>(ktot, 1) * 2 + 15) & ~(size_t)15);
+    if (!out->ref || !out->k || !out->rmsq || !out->block_off || !out->keys) {
+        pbf_keys_free(out);
+        return fail(PBF_E_IO, "out of host memory");
+    }
+    if (L) memcpy(out->ref, in->ref, L);
+    memcpy(out->k, in->k, nt * kb);
+    const uint16_t *src = in->keys + k0;   // offsets may be absolute (include/popbam_gpu.h)
+    uint64_t r = 0, nk = 0;
+    for (size_t t = 0; t < nt; ++t) {
+        if (t % ((size_t)64 * ns) == 0) out->block_off[t / ((size_t)64 * ns)] = nk;
+        const uint32_t kk = kb == 1 ? ((const uint8_t *)in->k)[t] : ((const uint16_t *)in->k)[t];
+        uint32_t rq = in->rmsq[t];
+        const uint8_t rc = in->ref[t / ns];
+        const int cb = !(rc & 0x80) ? ref_base_upper(rc) : -1;
+        if (rq >> 31) {
+            pbf_keys_free(out);
+            return fail(PBF_E_ARG, "a sum of mapQ^2 reaches bit 31: no compact form");
+        }
+        if (cb >= 0 && kk >= 1 && kk <= 32 && all_on_base(src + r, kk, (uint32_t)cb)) {
+            rq |= 0x80000000u;
+        } else {
+            memcpy(out->keys + nk, src + r, (size_t)kk * 2);
+            nk += kk;
+        }
+        r += kk;
+        out->rmsq[t] = rq;
+    }
+    if (r != ktot) {
+        pbf_keys_free(out);
+        return fail(PBF_E_ARG, "block_off does not add up to k[]");
+    }
+    out->block_off[nblk] = nk;
     out->n_keys = nk;
     return PBF_OK;
 }

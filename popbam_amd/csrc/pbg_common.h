@@ -365,6 +365,9 @@ struct Batch {
     // the batch has long runs of a lower-case / N reference (the host saw them): the scan then
     // settles its list mid-block instead of sending what overflows it to call_overflow_kernel
     int masked;
+    // compact pieces (pbg_stream_push_compact): rmsq bit 31 flags a reference-only task whose keys
+    // the batch leaves out; block_off counts the keys present
+    int compact;
     // PBG_BOUNDS builds only: keys the checks take off the end of the batch's range (the
     // positive control, PBG_BOUNDS_SELFTEST=1: the batch's last chunk counts as outside, so a
     // correct kernel trips the check and pbg_check must report it); 0 otherwise
@@ -406,6 +409,7 @@ constexpr int kErrRow = 128;     // packed rows
 constexpr int kErrBlock = 256;   // per-block bookkeeping: D.pend, D.blk_cnt, D.sites
 constexpr int kErrWords = 512;   // consensus words (cb_out)
 constexpr int kErrPool = 1024;   // statistics workspace (pool / ZnS lists)
+constexpr int kErrCompact = 2048;   // (every build) a compact piece flagged a task that cannot be reference-only
 #ifdef PBG_BOUNDS
 __device__ __forceinline__ bool store_guard(int *err, uint64_t idx, uint64_t chk, uint64_t lim, int bit) {
     if (idx >= chk) atomicOr(err, bit);

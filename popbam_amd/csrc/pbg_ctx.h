@@ -66,6 +66,7 @@ struct pbg_ctx {
     void *d_scantab = nullptr;   // pbg::ScanTab (call_scan_kernel's LDS image)
     int *d_err = nullptr;
     int scan_masked = 0;   // the next pbg_call_sites' Batch::masked (set by pbg_stream_push from the host reference)
+    int scan_compact = 0;  // the next pbg_call_sites' Batch::compact (set by pbg_stream_push_compact)
     std::string err;
     // per-pileup LDS staging capacity (keyed by block_off pointer and size), so repeated
     // calls on the same resident batch do not synchronise

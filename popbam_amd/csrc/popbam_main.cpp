@@ -705,7 +705,12 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
     const auto blocks = window_blocks(rbeg, rend, o.win_size, windowed, block_sites);
     if (blocks.empty()) return std::string();
     if (!param_err.empty()) throw Fatal{param_err};
-    const pbf_filter flt{o.min_baseQ, o.min_mapQ, (o.flag & BAM_ILLUMINA) ? 1 : 0, max_depth <= 255 ? 1 : 2};
+    // compact pieces (pbg_stream_push_compact: the reference-only tasks' keys stay on the host)
+    // for every command but snp -o 0, whose consensus words need every task's keys;
+    // POPBAM_COMPACT=0 pushes the full pieces
+    const bool compact = !(cmd == "snp" && o.output == 0) && max_depth <= 33025 && env_int("POPBAM_COMPACT", 1) != 0;
+    const pbf_filter flt{o.min_baseQ, o.min_mapQ, (o.flag & BAM_ILLUMINA) ? 1 : 0, max_depth <= 255 ? 1 : 2,
+                         compact ? 1 : 0};
     std::vector<const char *> sn, pn, rg;
     for (auto &s : sm.samples) sn.push_back(s.c_str());
     for (auto &s : sm.pops) pn.push_back(s.c_str());
@@ -802,7 +807,8 @@ std::string run(const std::string &cmd, const std::vector<std::string> &argv, in
         const long fault_at = env_int("POPBAM_FAULT_PUSH", 0);
         long pushes = 0;
         auto push = [&](const pbg_pileup &pl) {
-            return ++pushes == fault_at ? PBG_E_BATCH : pbg_stream_push(st, &pl);
+            if (++pushes == fault_at) return (int)PBG_E_BATCH;
+            return compact ? pbg_stream_push_compact(st, &pl) : pbg_stream_push(st, &pl);
         };
         for (pbf_keys &p : early) {
             const auto tp = Clock::now();

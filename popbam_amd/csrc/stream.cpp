@@ -483,9 +483,13 @@ int pbg_stream_open(pbg_ctx *c, const pbg_cmd *cmds, uint32_t n_cmd, int32_t pos
 
 namespace {
 
-int stream_push(pbg_stream *st, const pbg_pileup *pc) {
+int stream_push(pbg_stream *st, const pbg_pileup *pc, bool compact) {
     pbg_ctx *c = st->c;
     if (st->finished) return fail(c, PBG_E_ARG, "stream already finished");
+    if (compact && st->words) return fail(c, PBG_E_ARG, "compact pieces carry no keys for reference-only tasks: no consensus words (snp -o 0)");
+    // a compact piece flags a task in bit 31 of its sum mapQ^2, which no unflagged task may reach:
+    // at most 255^2 per read, so max_depth <= 33025
+    if (compact && c->dp.max_depth > 33025) return fail(c, PBG_E_ARG, "compact pieces need max_depth <= 33025");
     if (pc->n_sites == 0) return PBG_OK;
     if (!pc->ref || !pc->k || !pc->rmsq || !pc->keys) return fail(c, PBG_E_ARG, "null pileup array");
     if ((int64_t)pc->pos0 != (int64_t)st->pos0 + st->pushed) return fail(c, PBG_E_ARG, "pieces must be pushed in position order");
@@ -505,7 +509,8 @@ int stream_push(pbg_stream *st, const pbg_pileup *pc) {
             own[bk] = run;
             const size_t t1 = (size_t)std::min<uint32_t>(L, (bk + 1) * pbg::kSiteBlock) * n;
             for (size_t i = (size_t)bk * pbg::kSiteBlock * n; i < t1; ++i)
-                run += kb == 1 ? ((const uint8_t *)pc->k)[i] : ((const uint16_t *)pc->k)[i];
+                if (!compact || !(pc->rmsq[i] >> 31))   // a flagged task's keys are not in the piece
+                    run += kb == 1 ? ((const uint8_t *)pc->k)[i] : ((const uint16_t *)pc->k)[i];
         }
         own[nblk] = run;
         boff = own.data();
@@ -564,9 +569,11 @@ int stream_push(pbg_stream *st, const pbg_pileup *pc) {
         if ((rc = ev_pair(st, 1, c0, c1))) return st->rc = rc;
         HIPCHK(c, hipEventRecord(c0, b.comp));
         c->scan_masked = masked_reference(pc->ref + p0, cl) ? 1 : 0;
+        c->scan_compact = compact ? 1 : 0;
         c->cap_hint_keys = (int64_t)(boff[b1] - boff[b0]);
         rc = pbg_call_sites(c, &dp, (char *)b.d_rows + roff * rb, st->words ? b.d_cb + roff * n : nullptr, b.comp);
         c->scan_masked = 0;
+        c->scan_compact = 0;
         c->cap_hint_keys = -1;
         if (rc) return st->rc = rc;
         HIPCHK(c, hipEventRecord(c1, b.comp));
@@ -613,7 +620,15 @@ extern "C" {
 int pbg_stream_push(pbg_stream *st, const pbg_pileup *pc) {
     if (!st || !pc) return PBG_E_ARG;
     if (st->rc) return st->rc;
-    const int rc = stream_push(st, pc);
+    const int rc = stream_push(st, pc, false);
+    if (rc) st->rc = rc;
+    return rc;
+}
+
+int pbg_stream_push_compact(pbg_stream *st, const pbg_pileup *pc) {
+    if (!st || !pc) return PBG_E_ARG;
+    if (st->rc) return st->rc;
+    const int rc = stream_push(st, pc, true);
     if (rc) st->rc = rc;
     return rc;
 }

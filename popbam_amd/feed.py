@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "libpopbam_feed.so")
 
 EXPORTS = ["pbf_last_error", "pbf_open", "pbf_close", "pbf_header_text", "pbf_n_refs", "pbf_ref_name",
            "pbf_ref_len", "pbf_has_index", "pbf_pileup", "pbf_pileup_mt", "pbf_batch_free", "pbf_fasta_fetch", "pbf_free",
-           "pbf_pack", "pbf_keys_free", "pbf_pileup_keys_mt", "pbf_kstream_open", "pbf_kstream_next",
+           "pbf_pack", "pbf_keys_free", "pbf_compact", "pbf_pileup_keys_mt", "pbf_kstream_open", "pbf_kstream_next",
            "pbf_kstream_profile", "pbf_kstream_close"]
 
 PBF_E_RG = -4
@@ -44,12 +44,15 @@ class PbfProfile(C.Structure):
 
 
 class PbfFilter(C.Structure):
-    _fields_ = [("min_baseQ", C.c_int32), ("min_mapQ", C.c_int32), ("illumina", C.c_int32), ("k_bytes", C.c_int32)]
+    _fields_ = [("min_baseQ", C.c_int32), ("min_mapQ", C.c_int32), ("illumina", C.c_int32), ("k_bytes", C.c_int32),
+                ("compact", C.c_int32)]
 
 
-def make_filter(min_baseQ: int, min_mapQ: int, flag: int, max_depth: int) -> PbfFilter:
-    """call_base's per-read filters (popbam.cpp:266-281) and the k width for max_depth."""
-    return PbfFilter(min_baseQ & 0xFF, min_mapQ & 0xFF, 1 if flag & 0x02 else 0, 1 if max_depth <= 255 else 2)
+def make_filter(min_baseQ: int, min_mapQ: int, flag: int, max_depth: int, compact: bool = False) -> PbfFilter:
+    """call_base's per-read filters (popbam.cpp:266-281) and the k width for max_depth; compact:
+    pieces for pbg_stream_push_compact (reference-only tasks flagged in rmsq bit 31, no keys)."""
+    return PbfFilter(min_baseQ & 0xFF, min_mapQ & 0xFF, 1 if flag & 0x02 else 0, 1 if max_depth <= 255 else 2,
+                     1 if compact else 0)
 
 
 class FeedError(RuntimeError):
@@ -90,6 +93,7 @@ def load():
     lib.pbf_pack.argtypes = [P(PbfBatch), C.c_int, P(PbfFilter), P(PbfKeys)]
     lib.pbf_keys_free.argtypes = [P(PbfKeys)]
     lib.pbf_keys_free.restype = None
+    lib.pbf_compact.argtypes = [P(PbfKeys), C.c_int, C.c_int, P(PbfKeys)]
     lib.pbf_pileup_keys_mt.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int, C.c_int32, C.c_int32, C.c_int32,
                                        C.c_char_p,
                                        P(C.c_char_p), P(C.c_int32), C.c_int, C.c_int32, C.c_int, C.c_int, P(PbfFilter),
@@ -159,6 +163,31 @@ def pack(batch: dict, n_samples: int, flt: PbfFilter) -> dict:
     out = PbfKeys()
     _check(lib, lib.pbf_pack(C.byref(raw), n_samples, C.byref(flt), C.byref(out)))
     return _take_keys(lib, out, n_samples, flt.k_bytes)
+
+
+def compact(keys: dict, n_samples: int, k_bytes: int) -> dict:
+    """pbf_compact: a key batch ({'ref', 'k', 'rmsq', 'keys', 'block_off'}) in the compact form of
+    pbg_stream_push_compact (reference-only tasks: rmsq bit 31, keys left out)."""
+    lib = load()
+    L = len(keys["ref"])
+    ref = np.ascontiguousarray(keys["ref"], dtype=np.uint8)
+    k = np.ascontiguousarray(keys["k"], dtype=np.uint8 if k_bytes == 1 else np.uint16).reshape(-1)
+    rmsq = np.ascontiguousarray(keys["rmsq"], dtype=np.uint32).reshape(-1)
+    ks = np.ascontiguousarray(keys["keys"], dtype=np.uint16)
+    if ks.size == 0:
+        ks = np.zeros(1, np.uint16)
+    boff = np.ascontiguousarray(keys["block_off"], dtype=np.uint64)
+    src = PbfKeys()
+    src.n_sites, src.pos0 = L, int(keys.get("pos0", 0))
+    src.ref = ref.ctypes.data_as(C.POINTER(C.c_uint8))
+    src.k = k.ctypes.data
+    src.rmsq = rmsq.ctypes.data_as(C.POINTER(C.c_uint32))
+    src.block_off = boff.ctypes.data_as(C.POINTER(C.c_uint64))
+    src.keys = ks.ctypes.data_as(C.POINTER(C.c_uint16))
+    src.n_keys = int(boff[(L + 63) // 64] - boff[0])
+    out = PbfKeys()
+    _check(lib, lib.pbf_compact(C.byref(src), n_samples, k_bytes, C.byref(out)))
+    return _take_keys(lib, out, n_samples, k_bytes)
 
 
 class Bam:
