@@ -10,7 +10,7 @@ rm -rf $O/prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$R/$O/prof" -o run \
   -- python3 "$R/bench.py" --steps 20 --warmup 3 --cpu-sample 0 --cli-sample 0 > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; }
 python3 tools/kstats.py $O/prof/run_kernel_stats.csv | head -12
-bash tools/pmc_traffic.sh 2 r05g || exit 1
+bash tools/pmc_traffic.sh 2 r06 || exit 1
 for c in 3 4; do
   timeout -k 10 400 python bench.py --config $c --steps 2 --warmup 1 --cpu-sample 0 > $O/bench_c$c.json 2> $O/bench_c$c.err || { tail -5 $O/bench_c$c.err; exit 1; }
   python3 -c "import json; d=json.loads(open('$O/bench_c$c.json').read().strip().splitlines()[-1]); print('c$c', d['value'], d['ms_per_step'], d['roofline']['frac'], d['parity_sampled'], d['rows_crosscheck']['identical'])"

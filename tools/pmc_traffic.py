@@ -2,7 +2,7 @@
 """Per-launch HBM bytes of every kernel from rocprofv3 --pmc passes (FETCH_SIZE doubled: gfx950
 counts half of wide streaming reads, MI355X_MICROARCH.md; WRITE_SIZE as is), written as
 profiles/pmc_traffic_c<config>.json with the source hash of this tree (bench.source_hash) and
-the bench shape, plus a per-round copy under profiles/$PROFDIR (default r05/) and a copy under
+the bench shape, plus a per-round copy under profiles/$PROFDIR (default r06/) and a copy under
 the counter directory (gpurun_out/..., which a GPU box hands back).
 usage: pmc_traffic.py <pmc dir with p*/ passes> <tag> <bench args...>"""
 import collections
@@ -43,9 +43,9 @@ call = sum(kern.get(k, {}).get("hbm_bytes", 0) for k in bench.CALL_KERNELS)
 out = {"src_sha": bench.source_hash(), "config": args.config, "shape": shape, "tag": tag,
        "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py {' '.join(bargs)}, {tag}",
        "fetch_correction": 2.0, "call_stage_hbm_bytes": call, "kernels": kern}
-os.makedirs(os.path.join(REPO, "profiles", os.environ.get("PROFDIR", "r05")), exist_ok=True)
+os.makedirs(os.path.join(REPO, "profiles", os.environ.get("PROFDIR", "r06")), exist_ok=True)
 for path in (os.path.join(REPO, "profiles", f"pmc_traffic_c{args.config}.json"),
-             os.path.join(REPO, "profiles", os.environ.get("PROFDIR", "r05"), f"{tag}_pmc_traffic_c{args.config}.json"),
+             os.path.join(REPO, "profiles", os.environ.get("PROFDIR", "r06"), f"{tag}_pmc_traffic_c{args.config}.json"),
              os.path.join(root, f"pmc_traffic_c{args.config}.json")):
     with open(path, "w") as f:
         json.dump(out, f, indent=1)

@@ -17,4 +17,4 @@ for set in FETCH_SIZE WRITE_SIZE; do
 done
 python3 tools/pmc_summary.py "$D" > "$D/summary.txt" || exit 1
 python3 tools/pmc_traffic.py "$D" "$TAG" $ARGS || exit 1
-mkdir -p "profiles/${PROFDIR:-r05}"; cp "$D/summary.txt" "profiles/${PROFDIR:-r05}/${TAG}_pmc_hbm_summary_c$CFG.txt"
+mkdir -p "profiles/${PROFDIR:-r06}"; cp "$D/summary.txt" "profiles/${PROFDIR:-r06}/${TAG}_pmc_hbm_summary_c$CFG.txt"
