@@ -15,7 +15,7 @@
 #if defined(PBG_SLOW_NONET) || defined(PBG_ZNS_EXP) || defined(PBG_ZNS_SORT) || defined(PBG_ZNS_PRIO) || \
     defined(PBG_SCAN_WIDE_PASS) || defined(PBG_CALL_WAVES_PER_SIMD) || defined(PBG_SLOW_WG_PER_CU) ||      \
     defined(PBG_WIN_AHEAD) || defined(PBG_FAST_MAX) || defined(PBG_SYNTH_EXP) || defined(PBG_SCAN_EXP) || \
-    defined(PBG_SCAN_LDS_PAD)
+    defined(PBG_SCAN_LDS_PAD) || defined(PBG_ZNS_GROUPS)
 #error "an experiment switch is defined: build variants with tools/variant.sh (-DPBG_EXPERIMENT=1)"
 #endif
 #define PBG_BUILD_KIND (PBG_BOUNDS_KIND)

@@ -858,16 +858,16 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
 // ZnS (calc_zns, pop_ld.cpp:201-252) as producer / consumer.  The reference's value of a
 // (window, population) chain is one sequential double sum of r^2 over every pair (a, b), a < b,
 // of the population's variable sites, in pair order: V(V-1)/2 dependent additions.  A workgroup
-// owns C consecutive chains and has 64 + 16 C threads.  Wave 0 is the adder: lane c keeps chain
+// owns C consecutive chains and has 64 + 16 G C threads.  Wave 0 is the adder: lane c keeps chain
 // c's running double and, per round, adds the chain's next 16 values in pair order from an LDS
 // ring (eight 16-byte reads issued a round ahead, then 16 register adds: the dependent chain
-// never waits on another lane).  Producer group c (16 lanes) walks chain c a row step per round:
-// lane j computes r^2 of pair (a, b0 + j) from the popcounts of the two sites' masks and of their
+// never waits on another lane).  Producer group (c, h) (16 lanes, h < G = kZnsG) walks chain c a
+// row step per round, taking the rounds r with r % G == h: lane j computes r^2 of pair (a, b0 + j) from the popcounts of the two sites' masks and of their
 // intersection (the host's r^2 table); lanes past the row's end give +0.0, which leaves the sum
 // unchanged, so the adder sees the reference's exact sequence of additions.  Rounds run in
 // phases of kZnsR: while the adder sums phase k - 1 from one half of the ring, the producers
 // fill the other half with phase k; one workgroup barrier per phase.  A producer first walks the
-// phase's kZnsR pairs (register arithmetic), then issues all their list reads, then all their
+// phase's kZnsR / G pairs (register arithmetic), then issues all their list reads, then all their
 // table reads, so a phase costs two LDS latencies, not 2 kZnsR.
 //
 // Fast path (every population of at most 26 samples and every list of the workgroup within the
@@ -885,7 +885,15 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
 #ifndef PBG_ZNS_PRIO
 #define PBG_ZNS_PRIO 3
 #endif
-constexpr int kZnsMaxC = 60;                 // chains per workgroup (64 + 16 C <= 1024 threads)
+// Two 16-lane producer groups per chain (rounds dealt out in turn: group h takes rounds h, h + 2,
+// ...): the producers of a workgroup's longest chains had been the slower side of each phase
+// (configs[2] statistics 0.2105 -> 0.1975 ms, A/B in one call; four groups: 0.243 ms, fewer chains
+// per workgroup, more workgroups than two per CU)
+#ifndef PBG_ZNS_GROUPS
+#define PBG_ZNS_GROUPS 2
+#endif
+constexpr int kZnsG = PBG_ZNS_GROUPS;        // 16-lane producer groups per chain
+constexpr int kZnsMaxC = 60 / kZnsG;         // chains per workgroup (64 + 16 G C <= 1024 threads)
 constexpr int kZnsR = 8;                     // rounds per phase
 constexpr int kZnsRingStride = 18;           // doubles per (round, chain): 16 values + 2 pad (LDS banks)
 
@@ -1041,11 +1049,18 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
         return;
     }
     // ---- the producers: group c = (tid - 64) / 16 walks chain c, lane j takes pair (a, b0 + j)
-    const int p = tid - 64, j = p & 15, g = p >> 4, c = s_ord[g];
+    const int p = tid - 64, j = p & 15, g = (p >> 4) / kZnsG, h = (p >> 4) % kZnsG, c = s_ord[g];
     const ZnsChain z = s_ch[c];
     const long long my_rounds = zns_rounds(z.V);
     const int V = z.V, V1 = z.V - 1, np1 = z.np1, r2o = z.r2o, vm = max(V1, 0);
     int a = 0, b0 = 1;
+    auto step = [&]() {   // the next row step of the chain's pair walk
+        b0 += 16;
+        const bool nxt = b0 >= V;
+        a += nxt ? 1 : 0;
+        b0 = nxt ? a + 1 : b0;
+    };
+    for (int x = 0; x < h; ++x) step();   // group h takes rounds h, h + G, ...
     const uint32_t *lst = s_lst + c * cap;
     const uint32_t np1sq = (uint32_t)(np1 * np1);
     const M *L = reinterpret_cast<const M *>(z.list);
@@ -1055,50 +1070,49 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
         if (k < nphase && PBG_ZNS_EXP != 1 && __ballot(k * kZnsR < my_rounds) != 0) {   // (exp 1: producers idle)
             double *out = s_ring + (size_t)(k & 1) * kZnsR * rstride + (size_t)g * kZnsRingStride + j;
             // the phase's pairs first (pure VALU), then every load of the phase in flight at once
-            int pa[kZnsR], pb[kZnsR];
-            bool ok[kZnsR];
+            constexpr int R = kZnsR / kZnsG;   // this group's rounds of the phase
+            int pa[R], pb[R];
+            bool ok[R];
 #pragma unroll
-            for (int r = 0; r < kZnsR; ++r) {
+            for (int r = 0; r < R; ++r) {
                 pa[r] = a;
                 pb[r] = b0 + j;
                 ok[r] = (a < V1) & (pb[r] < V);
-                b0 += 16;
-                const bool nxt = b0 >= V;
-                a += nxt ? 1 : 0;
-                b0 = nxt ? a + 1 : b0;
-            }
-            double v[kZnsR];
-            if (fast) {
-                uint32_t ea[kZnsR], eb[kZnsR];
 #pragma unroll
-                for (int r = 0; r < kZnsR; ++r) {
+                for (int x = 0; x < kZnsG; ++x) step();
+            }
+            double v[R];
+            if (fast) {
+                uint32_t ea[R], eb[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
                     ea[r] = lst[min(pa[r], vm)];   // clamped, not selected: no branch (unused when !ok)
                     eb[r] = lst[min(pb[r], vm)];
                 }
 #pragma unroll
-                for (int r = 0; r < kZnsR; ++r) {
+                for (int r = 0; r < R; ++r) {
                     const int idx = r2o + (int)(__umul24(ea[r] >> 26, np1sq) + __umul24(eb[r] >> 26, (uint32_t)np1)) +
                                     __popc(ea[r] & eb[r] & 0x03FFFFFFu);
                     v[r] = s_r2t[ok[r] ? idx : r2_lds];
                 }
             } else if (V > 1) {   // (a chain without pairs may have no list at all)
-                M ta[kZnsR], tb[kZnsR];
+                M ta[R], tb[R];
 #pragma unroll
-                for (int r = 0; r < kZnsR; ++r) {
+                for (int r = 0; r < R; ++r) {
                     ta[r] = L[min(pa[r], vm)];
                     tb[r] = L[min(pb[r], vm)];
                 }
 #pragma unroll
-                for (int r = 0; r < kZnsR; ++r) {
+                for (int r = 0; r < R; ++r) {
                     const double x = tab[r2o + ((int)pc(ta[r]) * np1 + (int)pc(tb[r])) * np1 + (int)pc(ta[r] & tb[r])];
                     v[r] = ok[r] ? x : 0.0;
                 }
             } else {
 #pragma unroll
-                for (int r = 0; r < kZnsR; ++r) v[r] = 0.0;
+                for (int r = 0; r < R; ++r) v[r] = 0.0;
             }
 #pragma unroll
-            for (int r = 0; r < kZnsR; ++r) out[(size_t)r * rstride] = v[r];
+            for (int r = 0; r < R; ++r) out[(size_t)(r * kZnsG + h) * rstride] = v[r];
         }
         __syncthreads();
     }
@@ -1129,7 +1143,7 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
         }
         const int r2_lds = r2_total <= 4608 ? r2_total : 0;   // <= 36 KB of LDS
         const uint32_t chains = n_win * (uint32_t)P.npops;
-        // C chains per workgroup (64 + 16 C threads): two workgroups per CU when the chains allow
+        // C chains per workgroup (64 + 16 G C threads): two workgroups per CU when the chains allow
         // it (two barrier domains interleave on a CU: 0.229 against 0.233 ms of statistics with
         // one), and as many as the LDS budget holds with lists of up to 256 sites
         const size_t budget = 75 * 1024;   // LDS per workgroup: two per CU
@@ -1144,7 +1158,7 @@ hipError_t launch_window_stats(int rb, const DevParams &P, const DevTables &T, c
         const int compact = (max_pop <= 26 && r2_lds && cap >= 16) ? 1 : 0;
         if (!compact) cap = 0;
         const size_t lds = fixed + (size_t)C * cap * 4;
-        const dim3 g((chains + C - 1) / C), b(64 + 16 * C);
+        const dim3 g((chains + C - 1) / C), b(64 + 16 * kZnsG * C);
         if (rb == 16)
             hipLaunchKernelGGL(window_zns_kernel<M2>, g, b, lds, stream, P, T, n_win, A, r2_lds, C, cap, compact);
         else
