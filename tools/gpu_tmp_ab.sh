@@ -1,4 +1,4 @@
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
-POPBAM_GPU_LIB=$R/popbam_amd/variants/zg4/libpopbam_gpu.so timeout -k 10 600 python -u -m pytest tests/test_gpu_scale.py -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread -k "window_stats_match and n12" > gpurun_out/pytest_zns.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_zns.log; [ $rc -ne 0 ] && exit $rc
-AB="zg2 zg4" bash tools/gpu_bench_ab.sh
+timeout -k 10 600 python -u -m pytest tests/test_gpu_scale.py tests/test_gpu_mixed_quality.py tests/test_compact.py -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread -k "call_kernel or rows_only or soft_masked or inconsistent or mixed or compact" > gpurun_out/pytest_pre.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_pre.log; [ $rc -ne 0 ] && exit $rc
+AB="base fold" bash tools/gpu_bench_ab.sh
