@@ -685,6 +685,25 @@ def genome_rows_crosscheck(torch, ctx, gp, slot: int = 0) -> dict:
             "seconds": round(time.perf_counter() - t0, 2)}
 
 
+def zns_chain_floor(ld_snps, zns_ms: float | None = None) -> dict:
+    """The ZnS sum's dependency floor (calc_zns, pop_ld.cpp:201-252): each window's r^2 values are
+    added in the reference's pair order, one dependent f64 add after another, so the kernel cannot
+    finish before its longest chain has.  window_zns_kernel pads each row of pairs to 16 (its
+    rounds, zns_rounds in stats_kernel.hip); tools/ubench/fadd_chain.hip measures 7 cycles per
+    dependent v_add_f64 with the operands in registers.  V is the window's S column (ns, which is
+    the chain's variable-site count or one more)."""
+    v = int(ld_snps.max().item()) if ld_snps.numel() else 0
+    n = max(v - 1, 0)
+    q, r = divmod(n, 16)
+    rounds = (q + 1) * (8 * q + r)
+    adds = 16 * rounds
+    out = {"longest_chain_sites": v, "pairs": v * (v - 1) // 2, "adds_padded": adds,
+           "floor_ms_at_7_cycles_2p4GHz": round(adds * 7 / 2.4e9 * 1e3, 4)}
+    if zns_ms:
+        out["kernel_ms"] = round(zns_ms, 4)
+    return out
+
+
 def max_over_ranks(dist, x: float) -> float:
     """The slowest rank's time (gloo, on the host)."""
     if not dist:
@@ -1081,7 +1100,8 @@ def main():
                            "traffic_ratio": round(call_traffic / call_bytes, 4) if call_traffic else None},
             "window_stats": {"ms_serial": round(stats_ms, 4), "rows_bytes": stats_bytes,
                              "GBps": round(stats_bytes / (stats_ms * 1e-3) / 1e9, 2),
-                             "Msites_per_s_stats_only": round(args.sites / (stats_ms * 1e-3) / 1e6, 2)},
+                             "Msites_per_s_stats_only": round(args.sites / (stats_ms * 1e-3) / 1e6, 2),
+                             "zns_chain": zns_chain_floor(hp.out.t["ld_snps"])},
         }
         if world == 1:
             out["pcie_inclusive"] = pcie_rate(torch, layout_bytes - args.sites * n, elapsed / args.steps, args.sites)

@@ -877,7 +877,7 @@ __global__ __launch_bounds__(kBlockThreads) void window_ld_kernel(DevParams P, D
 // Otherwise the raw masks (u64 / two-word) are read from the list buffer in HBM / L2, the table
 // from LDS or HBM.
 #ifndef PBG_ZNS_EXP
-#define PBG_ZNS_EXP 0   // timing experiments only (wrong results): 1 producers idle, 2 adder idle
+#define PBG_ZNS_EXP 0   // timing experiments only (wrong results): bit 0 producers idle, bit 1 adder idle
 #endif
 #ifndef PBG_ZNS_SORT
 #define PBG_ZNS_SORT 1
@@ -1025,13 +1025,17 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
 #pragma unroll
                         for (int x = 0; x < 8; ++x) nv[x] = rg[(size_t)(r + 1) * (rstride / 2) + x];
                     }
-#if PBG_ZNS_EXP != 2   // (timing experiment 2: no adds)
+                    // the next round's eight reads stay ahead of this round's sixteen adds (left to
+                    // itself, the scheduler sank them to one or two adds before their first use)
+                    __builtin_amdgcn_sched_barrier(0);
+#if !(PBG_ZNS_EXP & 2)   // (timing experiment 2: no adds)
 #pragma unroll
                     for (int x = 0; x < 8; ++x) {
                         acc += v[x].x;
                         acc += v[x].y;
                     }
 #endif
+                    __builtin_amdgcn_sched_barrier(0);
                     if (r + 1 < kZnsR) {
 #pragma unroll
                         for (int x = 0; x < 8; ++x) v[x] = nv[x];
@@ -1067,7 +1071,7 @@ __global__ __launch_bounds__(1024) void window_zns_kernel(DevParams P, DevTables
     const double *tab = r2_lds ? s_r2t : T.r2;
     for (long long k = 0; k <= nphase; ++k) {
         // (a wave whose four chains are all past their last round skips the phase)
-        if (k < nphase && PBG_ZNS_EXP != 1 && __ballot(k * kZnsR < my_rounds) != 0) {   // (exp 1: producers idle)
+        if (k < nphase && !(PBG_ZNS_EXP & 1) && __ballot(k * kZnsR < my_rounds) != 0) {   // (exp 1: producers idle)
             double *out = s_ring + (size_t)(k & 1) * kZnsR * rstride + (size_t)g * kZnsRingStride + j;
             // the phase's pairs first (pure VALU), then every load of the phase in flight at once
             constexpr int R = kZnsR / kZnsG;   // this group's rounds of the phase
