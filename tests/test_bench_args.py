@@ -41,3 +41,20 @@ def test_traffic_split_bounds_the_hbm_share():
     s = bench.traffic_split(20_370_000_000, 3.4142)   # configs[2]: within what HBM can deliver
     assert s["infinity_cache_bytes_at_least"] == 0
     assert bench.traffic_split(None, 3.0) is None
+
+
+@pytest.mark.parametrize("v", [0, 1, 2, 3, 16, 17, 18, 33, 181, 400])
+def test_zns_chain_floor_counts_the_kernels_padded_adds(v):
+    """window_stats.zns_chain: the longest chain's dependent adds as window_zns_kernel issues them
+    (each row of pairs (a, a+1..V-1) padded to a multiple of 16: zns_rounds in stats_kernel.hip),
+    against a direct count over the rows."""
+    import torch
+
+    import bench
+    z = bench.zns_chain_floor(torch.tensor([3, v, 1], dtype=torch.int32))
+    assert z["longest_chain_sites"] == max(v, 3)
+    vv = max(v, 3)
+    rows = [vv - 1 - a for a in range(vv - 1)]              # row a holds pairs (a, a+1 .. V-1)
+    assert z["pairs"] == sum(rows)
+    assert z["adds_padded"] == sum(-(-r // 16) * 16 for r in rows)
+    assert z["floor_ms_at_7_cycles_2p4GHz"] == round(z["adds_padded"] * 7 / 2.4e9 * 1e3, 4)
