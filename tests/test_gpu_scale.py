@@ -326,6 +326,31 @@ def test_window_stats_match_oracle(gpu_lib, n, npops, layout, stat, cmd_id, outp
     ctx.close()
 
 
+@pytest.mark.parametrize("n,npops", [(12, 1), (24, 3)])
+def test_zns_chain_past_the_lds_list(gpu_lib, n, npops):
+    """A ZnS chain longer than window_zns_kernel's LDS list capacity (at most 4096 sites): its
+    workgroup leaves the compacted fast path (s_fits) for the raw masks in the list buffer while
+    the r^2 table stays in LDS -- a combination no population-size setting reaches (populations
+    of at most 26 samples are compacted; wider ones have tables too large for LDS).  One window
+    over the whole batch beside a 10 kb one (its own workgroup, fast path), against the oracle."""
+    import torch
+    from popbam_amd import workload
+    n_sites = 64 * 8000
+    ctx, params = _ctx(n, npops)
+    syn = workload.SynthPileup(ctx, n_sites, 10, SEED + 11 * n)
+    wins = [(0, n_sites), (1000, 11_000)]
+    hp = workload.HotPath(ctx, syn, wins, 0x004)
+    hp.step()
+    torch.cuda.synchronize()
+    ns = hp.out.t["ld_snps"].cpu().numpy().reshape(len(wins), npops)
+    assert ns[0].max() > 4096, "the long chain must exceed the LDS list capacity"
+    types, flags = harness.rows_to_sites(hp.rows.cpu().numpy(), ctx.row_bytes, n_sites, n)
+    gpu = _window_text(ctx, params, hp, 5, 0, wins)   # ld -o 0 (PBG_S_ZNS)
+    orc = _oracle_text(params, types, flags, 5, 0, wins)
+    assert gpu == orc
+    ctx.close()
+
+
 def _interleaved_params(n, npops):
     """Populations dealt round-robin over the samples (sample v -> population v % npops), so
     pairs v < u with pop(v) > pop(u) exist (the Dxy asymmetry, Appendix A.6)."""
